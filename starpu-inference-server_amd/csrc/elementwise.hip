@@ -1,0 +1,308 @@
+// HBM-bound kernels around the MFMA contractions (gfx950): layout ingest,
+// pooling, LayerNorm, BERT embedding gather + LN, ViT patchify/assembly.
+// All loads/stores are 16-byte vectors where the layout allows (G13).
+#include "spi_kernels.hpp"
+
+#include <algorithm>
+
+namespace spi {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T cvt(float v) { return static_cast<T>(v); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+int grid_for(size_t n, int block = 256, int cap = 8192) {
+  return (int)std::max<size_t>(1, std::min<size_t>((n + block - 1) / block, cap));
+}
+
+// NCHW fp32 -> NHWC (T) with channel padding; one thread per pixel.
+template <typename T>
+__global__ void ingest_kernel(const float* __restrict__ x, T* __restrict__ y, int B,
+                              int C, int H, int W, int cpad) {
+  const size_t npix = (size_t)B * H * W;
+  const size_t HW = (size_t)H * W;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npix;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / HW, hw = i - b * HW;
+    T* dst = y + i * cpad;
+    for (int c = 0; c < cpad; ++c)
+      dst[c] = c < C ? cvt<T>(x[(b * C + c) * HW + hw]) : cvt<T>(0.f);
+  }
+}
+
+// Max pool on NHWC; thread per (pixel, channel).
+template <typename T>
+__global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
+                               int W, int C, int OH, int OW, int k, int stride, int pad) {
+  const size_t n = (size_t)B * OH * OW * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    size_t r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    float m = -INFINITY;
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * stride - pad + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * stride - pad + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        m = fmaxf(m, static_cast<float>(x[(((size_t)b * H + ih) * W + iw) * C + c]));
+      }
+    }
+    y[i] = cvt<T>(m);
+  }
+}
+
+// Global average pool: thread per (b, c), sums HW in fp32.
+template <typename T>
+__global__ void avgpool_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int HW,
+                               int C) {
+  const size_t n = (size_t)B * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / C, c = i - b * C;
+    const T* p = x + b * HW * C + c;
+    float s = 0.f;
+    for (int j = 0; j < HW; ++j) s += static_cast<float>(p[(size_t)j * C]);
+    y[i] = cvt<T>(s / (float)HW);
+  }
+}
+
+// One wave per row, D <= 64*16.  Two-pass mean/variance in fp32 registers.
+template <typename T, int VPL>
+__device__ __forceinline__ void ln_row(const float (&v)[VPL], int D, const float* g,
+                                       const float* b, float eps, float* yf, T* yt,
+                                       int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) s += v[j];
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < D) {
+      const float t = v[j] - mean;
+      q += t * t;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < D) {
+      const float o = (v[j] - mean) * rstd * g[c] + b[c];
+      if (yf) yf[c] = o;
+      if (yt) yt[c] = cvt<T>(o);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
+                                                        const float* g, const float* b,
+                                                        float* yf, T* yt, int ldy,
+                                                        int rows, int D, float eps) {
+  constexpr int VPL = 16;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (size_t)row * ldx;
+  float v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < D ? xr[c] : 0.f;
+  }
+  ln_row<T, VPL>(v, D, g, b, eps, yf ? yf + (size_t)row * ldy : nullptr,
+                 yt ? yt + (size_t)row * ldy : nullptr, lane);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bert_embed_kernel(
+    const int64_t* ids, const float* word, const float* pos, const float* type0,
+    const float* g, const float* b, float* yf, T* yt, int B, int S, int D, int vocab,
+    float eps) {
+  constexpr int VPL = 16;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B * S) return;
+  const int s = row % S;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const float* w = word + (size_t)id * D;
+  const float* p = pos + (size_t)s * D;
+  float v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < D ? (w[c] + type0[c]) + p[c] : 0.f;
+  }
+  ln_row<T, VPL>(v, D, g, b, eps, yf + (size_t)row * D, yt ? yt + (size_t)row * D : nullptr,
+                 lane);
+}
+
+__global__ void mask_bias_kernel(const int64_t* mask, float* bias, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    bias[i] = mask[i] != 0 ? 0.f : -3.4028234663852886e38f;  // (1 - m) * finfo(f32).min
+}
+
+// ViT patchify: row (b, ph, pw), column c*ps*ps + kh*ps + kw (conv weight flatten order).
+template <typename T>
+__global__ void patchify_kernel(const float* __restrict__ x, T* __restrict__ y, int B,
+                                int C, int H, int W, int ps) {
+  const int GH = H / ps, GW = W / ps;
+  const int K = C * ps * ps;
+  const size_t n = (size_t)B * GH * GW * K;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const size_t row = i / K;
+    const int pw = (int)(row % GW);
+    const int ph = (int)((row / GW) % GH);
+    const int b = (int)(row / ((size_t)GW * GH));
+    const int c = k / (ps * ps);
+    const int kh = (k / ps) % ps, kw = k % ps;
+    y[i] = cvt<T>(x[(((size_t)b * C + c) * H + ph * ps + kh) * W + pw * ps + kw]);
+  }
+}
+
+__global__ void vit_assemble_kernel(const float* __restrict__ patches,
+                                    const float* __restrict__ cls,
+                                    const float* __restrict__ pos, float* __restrict__ x,
+                                    int B, int P, int D) {
+  const size_t n = (size_t)B * (P + 1) * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % D);
+    const size_t r = i / D;
+    const int t = (int)(r % (P + 1));
+    const int b = (int)(r / (P + 1));
+    const float v = t == 0 ? cls[c] : patches[((size_t)b * P + (t - 1)) * D + c];
+    x[i] = v + pos[(size_t)t * D + c];
+  }
+}
+
+template <typename T>
+__global__ void gather_rows_kernel(const float* __restrict__ x, T* __restrict__ y, int rows,
+                                   int stride_rows, int D) {
+  const size_t n = (size_t)rows * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / D, c = i - r * D;
+    y[i] = cvt<T>(x[r * stride_rows * D + c]);
+  }
+}
+
+__global__ void affine_kernel(const float* x, float* y, size_t n, float scale, float shift) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    y[i] = x[i] * scale + shift;
+}
+
+}  // namespace
+
+
+void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad, bool f16,
+                 hipStream_t s) {
+  const size_t n = (size_t)B * H * W;
+  if (f16)
+    hipLaunchKernelGGL((ingest_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (_Float16*)y, B, C, H, W, cpad);
+  else
+    hipLaunchKernelGGL((ingest_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (float*)y, B, C, H, W, cpad);
+}
+
+void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH, int OW, int k,
+                  int stride, int pad, bool f16, hipStream_t s) {
+  const size_t n = (size_t)B * OH * OW * C;
+  if (f16)
+    hipLaunchKernelGGL((maxpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
+                       (const _Float16*)x, (_Float16*)y, B, H, W, C, OH, OW, k, stride, pad);
+  else
+    hipLaunchKernelGGL((maxpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
+                       (const float*)x, (float*)y, B, H, W, C, OH, OW, k, stride, pad);
+}
+
+void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s) {
+  const size_t n = (size_t)B * C;
+  if (f16)
+    hipLaunchKernelGGL((avgpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
+                       (const _Float16*)x, (_Float16*)y, B, HW, C);
+  else
+    hipLaunchKernelGGL((avgpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
+                       (const float*)x, (float*)y, B, HW, C);
+}
+
+void layernorm(const float* x, int ldx, const float* g, const float* b, float* yf, void* yt,
+               int ldy, int rows, int D, float eps, bool f16, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (f16)
+    hipLaunchKernelGGL((layernorm_kernel<_Float16>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+                       (_Float16*)yt, ldy, rows, D, eps);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<float>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+                       (float*)yt, ldy, rows, D, eps);
+}
+
+void bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                const float* g, const float* b, float* yf, void* yt, int B, int S, int D,
+                int vocab, float eps, bool f16, hipStream_t s) {
+  const dim3 grid((B * S + 3) / 4);
+  if (f16)
+    hipLaunchKernelGGL((bert_embed_kernel<_Float16>), grid, dim3(256), 0, s, ids, word, pos,
+                       type0, g, b, yf, (_Float16*)yt, B, S, D, vocab, eps);
+  else
+    hipLaunchKernelGGL((bert_embed_kernel<float>), grid, dim3(256), 0, s, ids, word, pos,
+                       type0, g, b, yf, (float*)yt, B, S, D, vocab, eps);
+}
+
+void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s) {
+  hipLaunchKernelGGL(mask_bias_kernel, dim3(grid_for(n)), dim3(256), 0, s, mask, bias, n);
+}
+
+void patchify(const float* x, void* y, int B, int C, int H, int W, int ps, bool f16,
+              hipStream_t s) {
+  const size_t n = (size_t)B * C * H * W;
+  if (f16)
+    hipLaunchKernelGGL((patchify_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (_Float16*)y, B, C, H, W, ps);
+  else
+    hipLaunchKernelGGL((patchify_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (float*)y, B, C, H, W, ps);
+}
+
+void vit_assemble(const float* patches, const float* cls, const float* pos, float* x, int B,
+                  int P, int D, hipStream_t s) {
+  const size_t n = (size_t)B * (P + 1) * D;
+  hipLaunchKernelGGL(vit_assemble_kernel, dim3(grid_for(n)), dim3(256), 0, s, patches, cls,
+                     pos, x, B, P, D);
+}
+
+void gather_rows(const float* x, void* y, int rows, int stride_rows, int D, bool f16,
+                 hipStream_t s) {
+  const size_t n = (size_t)rows * D;
+  if (f16)
+    hipLaunchKernelGGL((gather_rows_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (_Float16*)y, rows, stride_rows, D);
+  else
+    hipLaunchKernelGGL((gather_rows_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+                       (float*)y, rows, stride_rows, D);
+}
+
+void affine(const float* x, float* y, size_t n, float scale, float shift, hipStream_t s) {
+  hipLaunchKernelGGL(affine_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n, scale, shift);
+}
+
+}  // namespace spi

@@ -1,0 +1,886 @@
+// Model replica: recognise -> fold -> pack -> upload; per-stream workspaces;
+// forward plans for ResNet (basic / bottleneck), BERT (post-LN) and ViT
+// (pre-LN).  Reference counterparts: model loading and per-device clones
+// (src/core/inference_runner.cpp:243-275), the forward that LibTorch runs
+// inside the codelet (src/core/starpu_setup.cpp:610), and the model graphs the
+// reference exports (models/import_resnet.py:25-73, models/import_vit.py:10-62,
+// models/import_bert-base-uncased.py:8-39).
+#include "model.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <stdexcept>
+
+namespace spi {
+
+#define SPI_HIP(x)                                                                  \
+  do {                                                                              \
+    hipError_t e__ = (x);                                                           \
+    if (e__ != hipSuccess)                                                          \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e__) + \
+                               " at " #x);                                          \
+  } while (0)
+
+namespace {
+
+using PMap = std::map<std::string, const spi_named_tensor*>;
+
+int64_t numel(const spi_named_tensor* t) {
+  int64_t n = 1;
+  for (int i = 0; i < t->ndim; ++i) n *= t->shape[i];
+  return n;
+}
+
+const float* fdata(const spi_named_tensor* t) {
+  if (t->dtype != SPI_DTYPE_F32)
+    throw std::runtime_error(std::string("parameter ") + t->name + " must be fp32");
+  return static_cast<const float*>(t->data);
+}
+
+const spi_named_tensor* need(const PMap& p, const std::string& k) {
+  auto it = p.find(k);
+  if (it == p.end()) throw std::runtime_error("missing parameter '" + k + "'");
+  return it->second;
+}
+
+bool has(const PMap& p, const std::string& k) { return p.count(k) != 0; }
+
+int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Workspace: activation buffers for one stream at max_batch.
+// ---------------------------------------------------------------------------
+struct Workspace {
+  std::vector<void*> bufs;
+  float* partial = nullptr;
+  float* mask_bias = nullptr;
+  bool has_mask = false;
+  std::map<int, hipGraphExec_t> graphs;
+  ~Workspace() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    for (void* b : bufs) (void)hipFree(b);
+    if (partial) (void)hipFree(partial);
+    if (mask_bias) (void)hipFree(mask_bias);
+  }
+};
+
+namespace {
+
+class Blob {
+ public:
+  size_t add(const void* src, size_t bytes) {
+    const size_t off = (data_.size() + 255) & ~size_t(255);
+    data_.resize(off + bytes);
+    if (src) std::memcpy(data_.data() + off, src, bytes);
+    return off;
+  }
+  char* at(size_t off) { return data_.data() + off; }
+  std::vector<char>& data() { return data_; }
+
+ private:
+  std::vector<char> data_;
+};
+
+Blob* g_blob = nullptr;  // only used during construction (single thread)
+
+// Pack a [N][K] fp32 matrix (row-major, K contiguous) into [Npad][Kpad] of the
+// compute type.  get(n, k) supplies element (n, k) in packed-k order.
+template <typename F>
+size_t pack_matrix(int N, int K, int Npad, int Kpad, bool f16, F get) {
+  const size_t es = f16 ? 2 : 4;
+  const size_t off = g_blob->add(nullptr, (size_t)Npad * Kpad * es);
+  char* dst = g_blob->at(off);
+  std::memset(dst, 0, (size_t)Npad * Kpad * es);
+  for (int n = 0; n < N; ++n)
+    for (int k = 0; k < K; ++k) {
+      const float v = get(n, k);
+      if (f16)
+        reinterpret_cast<_Float16*>(dst)[(size_t)n * Kpad + k] = static_cast<_Float16>(v);
+      else
+        reinterpret_cast<float*>(dst)[(size_t)n * Kpad + k] = v;
+    }
+  return off;
+}
+
+size_t pack_vec(const float* v, int n) { return g_blob->add(v, (size_t)n * sizeof(float)); }
+
+// Conv weight [Cout][Cin][KH][KW] (+ eval BN) -> folded [Npad][Kpad], k =
+// (kh*KW + kw)*cin_pad + c; bias' = beta - mean * gamma / sqrt(var + eps).
+ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
+                int cin_pad, bool f16, float bn_eps) {
+  const spi_named_tensor* wt = need(p, wname + ".weight");
+  if (wt->ndim != 4) throw std::runtime_error(wname + ".weight must be 4-D");
+  ConvW c;
+  c.cout = (int)wt->shape[0];
+  c.cin = (int)wt->shape[1];
+  c.kh = (int)wt->shape[2];
+  c.kw = (int)wt->shape[3];
+  c.stride = stride;
+  c.pad = c.kh / 2;
+  c.cin_pad = std::max(cin_pad, c.cin);
+  const int K = c.kh * c.kw * c.cin_pad;
+  c.kpad = round_up(K, 64);
+  c.npad = round_up(c.cout, 128);
+  std::vector<double> scale(c.cout, 1.0), shift(c.cout, 0.0);
+  if (!bn.empty()) {
+    const float* g = fdata(need(p, bn + ".weight"));
+    const float* b = fdata(need(p, bn + ".bias"));
+    const float* m = fdata(need(p, bn + ".running_mean"));
+    const float* v = fdata(need(p, bn + ".running_var"));
+    for (int o = 0; o < c.cout; ++o) {
+      const double s = (double)g[o] / std::sqrt((double)v[o] + (double)bn_eps);
+      scale[o] = s;
+      shift[o] = (double)b[o] - (double)m[o] * s;
+    }
+  } else if (has(p, wname + ".bias")) {
+    const float* b = fdata(need(p, wname + ".bias"));
+    for (int o = 0; o < c.cout; ++o) shift[o] = b[o];
+  }
+  const float* w = fdata(wt);
+  const int cin = c.cin, kh = c.kh, kw = c.kw, cp = c.cin_pad;
+  c.w = pack_matrix(c.cout, K, c.npad, c.kpad, f16, [&](int n, int k) -> float {
+    const int cell = k / cp, ci = k % cp;
+    if (ci >= cin) return 0.f;
+    const int y = cell / kw, x = cell % kw;
+    return (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
+  });
+  std::vector<float> bias(c.cout);
+  for (int o = 0; o < c.cout; ++o) bias[o] = (float)shift[o];
+  c.b = pack_vec(bias.data(), c.cout);
+  return c;
+}
+
+LinearW pack_linear(const float* w, const float* b, int N, int K, bool f16) {
+  LinearW L;
+  L.n = N;
+  L.k = K;
+  L.kpad = round_up(K, 64);
+  L.npad = round_up(N, 128);
+  L.w = pack_matrix(N, K, L.npad, L.kpad, f16,
+                    [&](int n, int k) { return w[(size_t)n * K + k]; });
+  std::vector<float> zeros;
+  if (!b) {
+    zeros.assign(N, 0.f);
+    b = zeros.data();
+    L.has_bias = false;
+  }
+  L.b = pack_vec(b, N);
+  return L;
+}
+
+LinearW pack_linear_named(const PMap& p, const std::string& name, bool f16) {
+  const spi_named_tensor* wt = need(p, name + ".weight");
+  if (wt->ndim != 2) throw std::runtime_error(name + ".weight must be 2-D");
+  const float* b = has(p, name + ".bias") ? fdata(need(p, name + ".bias")) : nullptr;
+  return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], f16);
+}
+
+LnW pack_ln(const PMap& p, const std::string& name) {
+  LnW l;
+  const spi_named_tensor* g = need(p, name + ".weight");
+  l.g = pack_vec(fdata(g), (int)numel(g));
+  l.b = pack_vec(fdata(need(p, name + ".bias")), (int)numel(g));
+  return l;
+}
+
+// Strip the common prefix in front of an anchor name ("bert.embeddings..." ->
+// "embeddings..."), so wrapped modules are recognised.
+PMap strip_prefix(const PMap& in, const std::string& anchor) {
+  std::string prefix;
+  bool found = false;
+  for (auto& kv : in) {
+    const std::string& k = kv.first;
+    if (k.size() >= anchor.size() && k.compare(k.size() - anchor.size(), anchor.size(), anchor) == 0) {
+      const std::string pre = k.substr(0, k.size() - anchor.size());
+      if (pre.empty() || pre.back() == '.') {
+        prefix = pre;
+        found = true;
+        break;
+      }
+    }
+  }
+  if (!found || prefix.empty()) return in;
+  PMap out;
+  for (auto& kv : in)
+    if (kv.first.compare(0, prefix.size(), prefix) == 0) out[kv.first.substr(prefix.size())] = kv.second;
+  return out;
+}
+
+bool ends_with(const PMap& p, const std::string& anchor) {
+  for (auto& kv : p) {
+    const std::string& k = kv.first;
+    if (k.size() >= anchor.size() && k.compare(k.size() - anchor.size(), anchor.size(), anchor) == 0)
+      return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Construction
+// ---------------------------------------------------------------------------
+Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* params, int n)
+    : device_(device), family_(cfg.family), f16_(cfg.precision == SPI_PREC_F16),
+      max_batch_(std::max(1, cfg.max_batch)) {
+  if (cfg.precision != SPI_PREC_F16 && cfg.precision != SPI_PREC_F32)
+    throw std::runtime_error("unsupported precision");
+  PMap p;
+  for (int i = 0; i < n; ++i) {
+    if (!params[i].name) throw std::runtime_error("parameter without a name");
+    p[params[i].name] = &params[i];
+  }
+  if (family_ == SPI_FAMILY_AUTO) {
+    if (ends_with(p, "embeddings.word_embeddings.weight")) family_ = SPI_FAMILY_BERT;
+    else if (ends_with(p, "conv_proj.weight") && ends_with(p, "class_token")) family_ = SPI_FAMILY_VIT;
+    else if (ends_with(p, "layer1.0.conv1.weight")) family_ = SPI_FAMILY_RESNET;
+    else throw std::runtime_error("unrecognised model: no ResNet/BERT/ViT parameter names");
+  }
+  Blob blob;
+  g_blob = &blob;
+  std::ostringstream os;
+  if (family_ == SPI_FAMILY_AFFINE) {
+    aff_scale_ = cfg.affine_scale;
+    aff_shift_ = cfg.affine_shift;
+    os << "affine(x*" << aff_scale_ << "+" << aff_shift_ << ") f32";
+  } else if (family_ == SPI_FAMILY_RESNET) {
+    if (cfg.image_size > 0) image_ = cfg.image_size;
+    eps_ = cfg.eps > 0 ? cfg.eps : 1e-5f;
+    build_resnet(strip_prefix(p, "layer1.0.conv1.weight"));
+    os << "resnet" << (bottleneck_ ? "-bottleneck[" : "-basic[");
+    for (size_t i = 0; i < stage_blocks_.size(); ++i) os << (i ? "," : "") << stage_blocks_[i];
+    os << "] img" << image_ << " classes" << classes_;
+  } else if (family_ == SPI_FAMILY_BERT) {
+    eps_ = cfg.eps > 0 ? cfg.eps : 1e-12f;
+    heads_ = cfg.num_heads;
+    seq_ = cfg.seq_len;
+    build_bert(strip_prefix(p, "embeddings.word_embeddings.weight"));
+    os << "bert L" << layers_ << " D" << D_ << " H" << heads_ << " FF" << ffn_ << " S<=" << seq_;
+  } else if (family_ == SPI_FAMILY_VIT) {
+    eps_ = cfg.eps > 0 ? cfg.eps : 1e-6f;
+    heads_ = cfg.num_heads;
+    if (cfg.image_size > 0) image_ = cfg.image_size;
+    build_vit(strip_prefix(p, "conv_proj.weight"));
+    os << "vit L" << layers_ << " D" << D_ << " H" << heads_ << " MLP" << ffn_ << " patch" << patch_
+       << " img" << image_ << " classes" << classes_;
+  } else {
+    throw std::runtime_error("unsupported model family");
+  }
+  os << (f16_ ? " f16" : " f32") << " maxB" << max_batch_;
+  desc_ = os.str();
+  g_blob = nullptr;
+
+  blob_bytes_ = blob.data().size();
+  if (device_ < 0) return;  // host-only replica: recognised and packed, never uploaded
+  SPI_HIP(hipSetDevice(device_));
+  if (blob_bytes_) {
+    SPI_HIP(hipMalloc(&dblob_, blob_bytes_));
+    SPI_HIP(hipMemcpy(dblob_, blob.data().data(), blob_bytes_, hipMemcpyHostToDevice));
+  }
+}
+
+Model::~Model() {
+  ws_.clear();
+  if (dblob_) (void)hipFree(dblob_);
+}
+
+void Model::build_resnet(const PMap& p) {
+  // Stages: torchvision layer1..layer4, stride 2 on the first block of 2..4
+  // (on conv1 for BasicBlock, conv2 for Bottleneck: torchvision v1.5).
+  bottleneck_ = has(p, "layer1.0.conv3.weight");
+  const int cin_pad = f16_ ? 8 : 4;
+  stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, f16_, eps_);
+  if (stem_.kh != 7 || stem_.cin != 3) throw std::runtime_error("resnet stem must be 7x7 over 3 channels");
+  for (int L = 1; L <= 4; ++L) {
+    int nb = 0;
+    while (has(p, "layer" + std::to_string(L) + "." + std::to_string(nb) + ".conv1.weight")) ++nb;
+    if (nb == 0) throw std::runtime_error("resnet layer" + std::to_string(L) + " missing");
+    stage_blocks_.push_back(nb);
+    for (int i = 0; i < nb; ++i) {
+      const std::string pre = "layer" + std::to_string(L) + "." + std::to_string(i) + ".";
+      const int s = (L > 1 && i == 0) ? 2 : 1;
+      ResBlock blk;
+      if (bottleneck_) {
+        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", 1, 0, f16_, eps_);
+        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", s, 0, f16_, eps_);
+        blk.c3 = pack_conv(p, pre + "conv3", pre + "bn3", 1, 0, f16_, eps_);
+      } else {
+        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", s, 0, f16_, eps_);
+        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", 1, 0, f16_, eps_);
+      }
+      blk.has_ds = has(p, pre + "downsample.0.weight");
+      if (blk.has_ds) blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, f16_, eps_);
+      blocks_.push_back(blk);
+    }
+  }
+  fc_ = pack_linear_named(p, "fc", f16_);
+  classes_ = fc_.n;
+  feat_ = fc_.k;
+  for (auto& b : blocks_) {
+    const ConvW* cs[] = {&b.c1, &b.c2, &b.c3, &b.ds};
+    for (const ConvW* c : cs)
+      if (c->cout && (c->cin_pad % 8 != 0 || (c->cin_pad & (c->cin_pad - 1))))
+        throw std::runtime_error("resnet conv channels must be a power of two >= 8");
+  }
+}
+
+void Model::build_bert(const PMap& p) {
+  const spi_named_tensor* we = need(p, "embeddings.word_embeddings.weight");
+  vocab_ = (int)we->shape[0];
+  D_ = (int)we->shape[1];
+  const spi_named_tensor* pe = need(p, "embeddings.position_embeddings.weight");
+  maxpos_ = (int)pe->shape[0];
+  if (heads_ <= 0) heads_ = D_ / 64;
+  if (D_ % heads_ != 0 || D_ / heads_ != 64) throw std::runtime_error("attention head_dim must be 64");
+  if (D_ % 64 != 0 || D_ > 1024) throw std::runtime_error("hidden size must be a multiple of 64, <= 1024");
+  if (seq_ <= 0) seq_ = maxpos_;
+  word_ = pack_vec(fdata(we), (int)numel(we));
+  pos_ = pack_vec(fdata(pe), (int)numel(pe));
+  const spi_named_tensor* te = need(p, "embeddings.token_type_embeddings.weight");
+  type0_ = pack_vec(fdata(te), D_);  // token_type_ids buffer is all zeros
+  emb_ln_ = pack_ln(p, "embeddings.LayerNorm");
+  while (has(p, "encoder.layer." + std::to_string(layers_) + ".attention.self.query.weight")) ++layers_;
+  if (layers_ == 0) throw std::runtime_error("bert: no encoder layers");
+  for (int i = 0; i < layers_; ++i) {
+    const std::string pre = "encoder.layer." + std::to_string(i) + ".";
+    TfLayer L;
+    // Q, K, V stacked into one [3D][D] projection.
+    std::vector<float> w((size_t)3 * D_ * D_), b((size_t)3 * D_);
+    const char* names[3] = {"query", "key", "value"};
+    for (int j = 0; j < 3; ++j) {
+      const std::string nm = pre + "attention.self." + names[j];
+      std::memcpy(w.data() + (size_t)j * D_ * D_, fdata(need(p, nm + ".weight")), sizeof(float) * D_ * D_);
+      std::memcpy(b.data() + (size_t)j * D_, fdata(need(p, nm + ".bias")), sizeof(float) * D_);
+    }
+    L.qkv = pack_linear(w.data(), b.data(), 3 * D_, D_, f16_);
+    L.out = pack_linear_named(p, pre + "attention.output.dense", f16_);
+    L.ln1 = pack_ln(p, pre + "attention.output.LayerNorm");
+    L.ff1 = pack_linear_named(p, pre + "intermediate.dense", f16_);
+    L.ff2 = pack_linear_named(p, pre + "output.dense", f16_);
+    L.ln2 = pack_ln(p, pre + "output.LayerNorm");
+    ffn_ = L.ff1.n;
+    tf_.push_back(L);
+  }
+}
+
+void Model::build_vit(const PMap& p) {
+  const spi_named_tensor* cw = need(p, "conv_proj.weight");
+  D_ = (int)cw->shape[0];
+  patch_ = (int)cw->shape[2];
+  if (cw->shape[1] != 3 || cw->shape[3] != patch_) throw std::runtime_error("vit conv_proj must be PxP over 3 channels");
+  if (image_ % patch_) throw std::runtime_error("image size must be a multiple of the patch size");
+  npatch_ = (image_ / patch_) * (image_ / patch_);
+  if (heads_ <= 0) heads_ = D_ / 64;
+  if (D_ % heads_ != 0 || D_ / heads_ != 64) throw std::runtime_error("attention head_dim must be 64");
+  if (D_ % 64 != 0 || D_ > 1024) throw std::runtime_error("hidden size must be a multiple of 64, <= 1024");
+  const int K = 3 * patch_ * patch_;
+  patch_proj_ = pack_linear(fdata(cw), has(p, "conv_proj.bias") ? fdata(need(p, "conv_proj.bias")) : nullptr,
+                            D_, K, f16_);
+  cls_ = pack_vec(fdata(need(p, "class_token")), D_);
+  const spi_named_tensor* pe = need(p, "encoder.pos_embedding");
+  if (numel(pe) != (int64_t)(npatch_ + 1) * D_) throw std::runtime_error("pos_embedding does not match image/patch size");
+  vpos_ = pack_vec(fdata(pe), (int)numel(pe));
+  while (has(p, "encoder.layers.encoder_layer_" + std::to_string(layers_) + ".ln_1.weight")) ++layers_;
+  if (layers_ == 0) throw std::runtime_error("vit: no encoder layers");
+  for (int i = 0; i < layers_; ++i) {
+    const std::string pre = "encoder.layers.encoder_layer_" + std::to_string(i) + ".";
+    TfLayer L;
+    L.ln1 = pack_ln(p, pre + "ln_1");
+    const spi_named_tensor* iw = need(p, pre + "self_attention.in_proj_weight");
+    L.qkv = pack_linear(fdata(iw), fdata(need(p, pre + "self_attention.in_proj_bias")), (int)iw->shape[0],
+                        (int)iw->shape[1], f16_);
+    L.out = pack_linear_named(p, pre + "self_attention.out_proj", f16_);
+    L.ln2 = pack_ln(p, pre + "ln_2");
+    const std::string m1 = has(p, pre + "mlp.0.weight") ? pre + "mlp.0" : pre + "mlp.linear_1";
+    const std::string m2 = has(p, pre + "mlp.3.weight") ? pre + "mlp.3" : pre + "mlp.linear_2";
+    L.ff1 = pack_linear_named(p, m1, f16_);
+    L.ff2 = pack_linear_named(p, m2, f16_);
+    ffn_ = L.ff1.n;
+    tf_.push_back(L);
+  }
+  final_ln_ = pack_ln(p, "encoder.ln");
+  head_ = pack_linear_named(p, "heads.head", f16_);
+  classes_ = head_.n;
+  seq_ = npatch_ + 1;
+}
+
+// ---------------------------------------------------------------------------
+// I/O contract
+// ---------------------------------------------------------------------------
+size_t Model::out_elems_per_sample() const {
+  switch (family_) {
+    case SPI_FAMILY_RESNET:
+    case SPI_FAMILY_VIT:
+      return (size_t)classes_;
+    case SPI_FAMILY_BERT:
+      return 0;  // depends on S: checked in check_io
+    default:
+      return 0;
+  }
+}
+
+int Model::num_inputs_min() const { return 1; }
+int Model::num_inputs_max() const { return family_ == SPI_FAMILY_BERT ? 2 : 1; }
+
+void Model::check_io(const spi_codelet_args& a, const size_t* in_bytes, const size_t* out_bytes) const {
+  const int ni = (int)a.num_inputs, no = (int)a.num_outputs;
+  if (ni < num_inputs_min() || ni > num_inputs_max())
+    throw std::runtime_error("model expects " + std::to_string(num_inputs_max()) + " input(s), got " +
+                             std::to_string(ni));
+  if (no != 1) throw std::runtime_error("Mismatch between model outputs and StarPU buffers");
+  const int64_t B = a.dims[0][0];
+  if (B < 1 || B > max_batch_)
+    throw std::runtime_error("batch " + std::to_string(B) + " exceeds replica max_batch " +
+                             std::to_string(max_batch_));
+  auto elems = [&](int i) {
+    int64_t e = 1;
+    for (int d = 0; d < a.num_dims[i]; ++d) e *= a.dims[i][d];
+    return e;
+  };
+  size_t expect_out = 0;
+  if (family_ == SPI_FAMILY_AFFINE) {
+    if (a.input_types[0] != SPI_DTYPE_F32) throw std::runtime_error("[ERROR] Input type mismatch");
+    if (in_bytes[0] < (size_t)elems(0) * 4) throw std::runtime_error("[ERROR] Input buffer too small");
+    expect_out = (size_t)elems(0) * 4;
+  } else if (family_ == SPI_FAMILY_RESNET || family_ == SPI_FAMILY_VIT) {
+    if (a.input_types[0] != SPI_DTYPE_F32) throw std::runtime_error("[ERROR] Input type mismatch");
+    if (a.num_dims[0] != 4 || a.dims[0][1] != 3 || a.dims[0][2] != image_ || a.dims[0][3] != image_)
+      throw std::runtime_error("[ERROR] Tensor layout mismatch: expected [B,3," + std::to_string(image_) + "," +
+                               std::to_string(image_) + "]");
+    if (in_bytes[0] < (size_t)elems(0) * 4) throw std::runtime_error("[ERROR] Input buffer too small");
+    expect_out = (size_t)B * classes_ * 4;
+  } else {  // BERT: input_ids [B,S] int64, optional attention_mask [B,S] int64
+    for (int i = 0; i < ni; ++i) {
+      if (a.input_types[i] != SPI_DTYPE_I64) throw std::runtime_error("[ERROR] Input type mismatch");
+      if (a.num_dims[i] != 2 || a.dims[i][0] != B || a.dims[i][1] != a.dims[0][1])
+        throw std::runtime_error("[ERROR] Tensor layout mismatch");
+      if (in_bytes[i] < (size_t)elems(i) * 8) throw std::runtime_error("[ERROR] Input buffer too small");
+    }
+    const int64_t S = a.dims[0][1];
+    if (S < 1 || S > seq_ || S > maxpos_)
+      throw std::runtime_error("sequence length " + std::to_string(S) + " exceeds " + std::to_string(seq_));
+    expect_out = (size_t)B * S * D_ * 4;
+  }
+  if (a.output_types[0] != SPI_DTYPE_F32) throw std::runtime_error("[ERROR] Output type mismatch");
+  if (out_bytes[0] != expect_out) throw std::runtime_error("Output buffer size mismatch in bytes");
+}
+
+double Model::flops(int64_t B) const {
+  double f = 0;
+  auto conv_f = [&](const ConvW& c, int OH, int OW) {
+    return 2.0 * B * OH * OW * c.cout * (double)c.kh * c.kw * c.cin;
+  };
+  if (family_ == SPI_FAMILY_RESNET) {
+    int H = (image_ + 2 * 3 - 7) / 2 + 1;
+    f += conv_f(stem_, H, H);
+    H = (H + 2 - 3) / 2 + 1;
+    for (const auto& b : blocks_) {
+      if (bottleneck_) {
+        f += conv_f(b.c1, H, H);
+        const int H2 = (H + 2 * b.c2.pad - b.c2.kh) / b.c2.stride + 1;
+        f += conv_f(b.c2, H2, H2) + conv_f(b.c3, H2, H2);
+        if (b.has_ds) f += conv_f(b.ds, H2, H2);
+        H = H2;
+      } else {
+        const int H2 = (H + 2 * b.c1.pad - b.c1.kh) / b.c1.stride + 1;
+        f += conv_f(b.c1, H2, H2) + conv_f(b.c2, H2, H2);
+        if (b.has_ds) f += conv_f(b.ds, H2, H2);
+        H = H2;
+      }
+    }
+    f += 2.0 * B * fc_.n * fc_.k;
+  } else if (family_ == SPI_FAMILY_BERT || family_ == SPI_FAMILY_VIT) {
+    const double S = family_ == SPI_FAMILY_BERT ? seq_ : npatch_ + 1;
+    const double T = B * S;
+    for (const auto& L : tf_)
+      f += 2.0 * T * ((double)L.qkv.n * L.qkv.k + (double)L.out.n * L.out.k + (double)L.ff1.n * L.ff1.k +
+                      (double)L.ff2.n * L.ff2.k) +
+           4.0 * B * S * S * D_;
+    if (family_ == SPI_FAMILY_VIT) f += 2.0 * B * npatch_ * (double)D_ * patch_proj_.k + 2.0 * B * head_.n * head_.k;
+  }
+  return f;
+}
+
+// ---------------------------------------------------------------------------
+// Launch helpers
+// ---------------------------------------------------------------------------
+namespace {
+GemmDesc conv_desc(const ConvW& c, int B, int H, int W, int& OH, int& OW) {
+  OH = (H + 2 * c.pad - c.kh) / c.stride + 1;
+  OW = (W + 2 * c.pad - c.kw) / c.stride + 1;
+  GemmDesc d;
+  d.M = B * OH * OW;
+  d.N = c.cout;
+  d.K = c.kh * c.kw * c.cin_pad;
+  d.Kpad = c.kpad;
+  d.ldc = c.cout;
+  d.ldr = c.cout;
+  d.conv = true;
+  d.H = H;
+  d.W = W;
+  d.Cin = c.cin_pad;
+  d.OH = OH;
+  d.OW = OW;
+  d.KH = c.kh;
+  d.KW = c.kw;
+  d.stride = c.stride;
+  d.pad = c.pad;
+  return d;
+}
+
+GemmDesc linear_desc(const LinearW& L, int M, int lda, int ldc) {
+  GemmDesc d;
+  d.M = M;
+  d.N = L.n;
+  d.K = L.k;
+  d.Kpad = L.kpad;
+  d.lda = lda;
+  d.ldc = ldc;
+  d.ldr = ldc;
+  return d;
+}
+}  // namespace
+
+size_t Model::conv_partial(const ConvW& c, int B, int H, int W) const {
+  int OH, OW;
+  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW), f16_);
+}
+
+size_t Model::linear_partial(const LinearW& L, int M) const {
+  return gemm_partial_floats(linear_desc(L, M, L.k, L.n), f16_);
+}
+
+void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
+                     Act act, const void* res, float* partial, hipStream_t s) {
+  GemmDesc d = conv_desc(c, B, H, W, OH, OW);
+  d.act = act;
+  const size_t es = f16_ ? 2 : 4;
+  if (prof_)
+    op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
+                    std::to_string(c.cout) + "_s" + std::to_string(c.stride) + "_M" + std::to_string(d.M),
+             2.0 * d.M * d.N * (double)c.kh * c.kw * c.cin,
+             (double)B * H * W * c.cin_pad * es + (double)c.cout * d.K * es + (double)d.M * d.N * es * (res ? 2 : 1));
+  GemmPtrs p;
+  p.A = x;
+  p.W = ptr<void>(c.w);
+  p.bias = ptr<float>(c.b);
+  p.res = res;
+  p.C = y;
+  p.partial = partial;
+  gemm(d, p, f16_, s);
+  if (prof_) op_end(s);
+}
+
+void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc, bool out_f32, Act act,
+                     const void* res, bool res_f32, int ldr, float* partial, hipStream_t s) {
+  GemmDesc d = linear_desc(L, M, lda, ldc);
+  d.act = act;
+  d.out_f32 = out_f32;
+  d.res_f32 = res_f32;
+  d.ldr = ldr;
+  const size_t es = f16_ ? 2 : 4;
+  if (prof_)
+    op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
+             2.0 * M * L.n * (double)L.k,
+             (double)M * L.k * es + (double)L.n * L.k * es + (double)M * L.n * (out_f32 ? 4 : es) +
+                 (res ? (double)M * L.n * (res_f32 ? 4 : es) : 0.0));
+  GemmPtrs p;
+  p.A = A;
+  p.W = ptr<void>(L.w);
+  p.bias = ptr<float>(L.b);
+  p.res = res;
+  p.C = C;
+  p.partial = partial;
+  gemm(d, p, f16_, s);
+  if (prof_) op_end(s);
+}
+
+// ---------------------------------------------------------------------------
+// Workspaces
+// ---------------------------------------------------------------------------
+Workspace* Model::workspace(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = ws_.find(s);
+  if (it != ws_.end()) return it->second.get();
+  auto w = std::make_unique<Workspace>();
+  const size_t es = f16_ ? 2 : 4;
+  const int B = max_batch_;
+  size_t partial = 0;
+  std::vector<size_t> sizes;  // bytes per buffer
+  if (family_ == SPI_FAMILY_RESNET) {
+    const int cp = stem_.cin_pad;
+    sizes.push_back((size_t)B * image_ * image_ * cp * es);  // ingest
+    int H = image_, OH, OW;
+    size_t amax = 0;
+    partial = std::max(partial, conv_partial(stem_, B, H, H));
+    conv_desc(stem_, B, H, H, OH, OW);
+    H = OH;
+    amax = std::max(amax, (size_t)B * H * H * stem_.cout);
+    H = (H + 2 - 3) / 2 + 1;
+    for (const auto& b : blocks_) {
+      int H2;
+      if (bottleneck_) {
+        partial = std::max(partial, conv_partial(b.c1, B, H, H));
+        amax = std::max(amax, (size_t)B * H * H * b.c1.cout);
+        partial = std::max(partial, conv_partial(b.c2, B, H, H));
+        conv_desc(b.c2, B, H, H, H2, OW);
+        amax = std::max(amax, (size_t)B * H2 * H2 * b.c2.cout);
+        partial = std::max(partial, conv_partial(b.c3, B, H2, H2));
+        amax = std::max(amax, (size_t)B * H2 * H2 * b.c3.cout);
+      } else {
+        partial = std::max(partial, conv_partial(b.c1, B, H, H));
+        conv_desc(b.c1, B, H, H, H2, OW);
+        amax = std::max(amax, (size_t)B * H2 * H2 * b.c1.cout);
+        partial = std::max(partial, conv_partial(b.c2, B, H2, H2));
+      }
+      if (b.has_ds) {
+        partial = std::max(partial, conv_partial(b.ds, B, H, H));
+        amax = std::max(amax, (size_t)B * H2 * H2 * b.ds.cout);
+      }
+      H = H2;
+    }
+    partial = std::max(partial, linear_partial(fc_, B));
+    for (int i = 0; i < 5; ++i) sizes.push_back(amax * es);
+    sizes.push_back((size_t)B * feat_ * es);  // pooled
+  } else if (family_ == SPI_FAMILY_BERT) {
+    const size_t T = (size_t)B * seq_;
+    sizes = {T * D_ * 4, T * D_ * es, T * 3 * D_ * es, T * D_ * es, T * D_ * 4, T * ffn_ * es};
+    for (const auto& L : tf_)
+      partial = std::max({partial, linear_partial(L.qkv, (int)T), linear_partial(L.out, (int)T),
+                          linear_partial(L.ff1, (int)T), linear_partial(L.ff2, (int)T)});
+    SPI_HIP(hipMalloc(&w->mask_bias, (size_t)B * seq_ * sizeof(float)));
+  } else if (family_ == SPI_FAMILY_VIT) {
+    const size_t S = npatch_ + 1, T = (size_t)B * S;
+    sizes = {(size_t)B * npatch_ * patch_proj_.k * es,  // 0 patches
+             (size_t)B * npatch_ * D_ * 4,              // 1 projected patches f32
+             T * D_ * 4,                                // 2 residual stream x f32
+             T * D_ * es,                               // 3 LN output
+             T * 3 * D_ * es,                           // 4 qkv
+             T * D_ * es,                               // 5 ctx
+             T * ffn_ * es,                             // 6 mlp hidden
+             (size_t)B * D_ * es};                      // 7 cls
+    partial = std::max(partial, linear_partial(patch_proj_, B * npatch_));
+    for (const auto& L : tf_)
+      partial = std::max({partial, linear_partial(L.qkv, (int)T), linear_partial(L.out, (int)T),
+                          linear_partial(L.ff1, (int)T), linear_partial(L.ff2, (int)T)});
+    partial = std::max(partial, linear_partial(head_, B));
+  }
+  for (size_t bytes : sizes) {
+    void* b = nullptr;
+    SPI_HIP(hipMalloc(&b, std::max<size_t>(bytes, 256)));
+    w->bufs.push_back(b);
+  }
+  if (partial) SPI_HIP(hipMalloc(&w->partial, partial * sizeof(float)));
+  Workspace* raw = w.get();
+  ws_[s] = std::move(w);
+  return raw;
+}
+
+// ---------------------------------------------------------------------------
+// Forward: prologue (reads the task's input buffers) -> body (workspace only,
+// graph-capturable) -> epilogue (writes the task's output buffer).
+// ---------------------------------------------------------------------------
+void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStream_t s) {
+  if (family_ == SPI_FAMILY_RESNET) {
+    ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
+  } else if (family_ == SPI_FAMILY_BERT) {
+    bert_embed(static_cast<const int64_t*>(in[0]), ptr<float>(word_), ptr<float>(pos_), ptr<float>(type0_),
+               ptr<float>(emb_ln_.g), ptr<float>(emb_ln_.b), static_cast<float*>(w.bufs[0]),
+               f16_ ? w.bufs[1] : nullptr, B, S, D_, vocab_, eps_, f16_, s);
+    w.has_mask = in[1] != nullptr;
+    if (w.has_mask) mask_to_bias(static_cast<const int64_t*>(in[1]), w.mask_bias, B * S, s);
+  } else if (family_ == SPI_FAMILY_VIT) {
+    patchify(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, patch_, f16_, s);
+  }
+}
+
+void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
+  if (family_ == SPI_FAMILY_RESNET) {
+    int H = image_, OH, OW;
+    void* const* buf = w.bufs.data();
+    run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w.partial, s);
+    H = OH;
+    const int PH = (H + 2 - 3) / 2 + 1;
+    maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    H = PH;
+    int cur = 2;
+    auto pick = [&](std::initializer_list<int> busy) {
+      for (int i = 1; i <= 5; ++i)
+        if (std::find(busy.begin(), busy.end(), i) == busy.end()) return i;
+      return -1;
+    };
+    for (const auto& b : blocks_) {
+      int H2;
+      if (bottleneck_) {
+        const int t1 = pick({cur});
+        run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w.partial, s);
+        const int t2 = pick({cur, t1});
+        run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w.partial, s);
+        int ident = cur;
+        if (b.has_ds) {
+          ident = pick({cur, t2});
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w.partial, s);
+        }
+        const int o = pick({cur, t2, ident});
+        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w.partial, s);
+        cur = o;
+      } else {
+        const int t1 = pick({cur});
+        run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w.partial, s);
+        int ident = cur;
+        if (b.has_ds) {
+          ident = pick({cur, t1});
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w.partial, s);
+        }
+        const int o = pick({cur, t1, ident});
+        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w.partial, s);
+        cur = o;
+      }
+      H = H2;
+    }
+    avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+  } else if (family_ == SPI_FAMILY_BERT) {
+    const int S = S_in, T = B * S;
+    float* hf = static_cast<float*>(w.bufs[0]);
+    void* ht = f16_ ? w.bufs[1] : w.bufs[0];
+    void* qkv = w.bufs[2];
+    void* ctx = w.bufs[3];
+    float* a = static_cast<float*>(w.bufs[4]);
+    void* ff = w.bufs[5];
+    const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
+    for (int i = 0; i < layers_; ++i) {
+      const TfLayer& L = tf_[i];
+      run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w.partial, s);
+      if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
+      attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
+      if (prof_) op_end(s);
+      run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w.partial, s);
+      layernorm(a, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_, s);
+      run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w.partial, s);
+      run_gemm(L.ff2, ff, T, ffn_, a, D_, true, Act::None, hf, true, D_, w.partial, s);
+      if (i + 1 < layers_)
+        layernorm(a, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_,
+                  s);
+    }
+  } else if (family_ == SPI_FAMILY_VIT) {
+    const int S = npatch_ + 1, T = B * S;
+    void* const* buf = w.bufs.data();
+    float* x = static_cast<float*>(buf[2]);
+    run_gemm(patch_proj_, buf[0], B * npatch_, patch_proj_.k, buf[1], D_, true, Act::None, nullptr, false, 0,
+             w.partial, s);
+    vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
+    const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
+    for (const TfLayer& L : tf_) {
+      layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
+                f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w.partial, s);
+      if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
+      attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
+      if (prof_) op_end(s);
+      run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w.partial, s);
+      layernorm(x, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
+                f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w.partial, s);
+      run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w.partial, s);
+    }
+    // final LN on the class-token rows only (torchvision: x = ln(x); x = x[:, 0])
+    layernorm(x, S * D_, ptr<float>(final_ln_.g), ptr<float>(final_ln_.b),
+              f16_ ? nullptr : static_cast<float*>(buf[7]), f16_ ? buf[7] : nullptr, D_, B, D_, eps_, f16_, s);
+  }
+}
+
+void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s) {
+  if (family_ == SPI_FAMILY_RESNET) {
+    run_gemm(fc_, w.bufs[6], B, feat_, out[0], classes_, true, Act::None, nullptr, false, 0, w.partial, s);
+  } else if (family_ == SPI_FAMILY_BERT) {
+    const TfLayer& L = tf_.back();
+    const int T = B * S;
+    layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
+              static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
+  } else if (family_ == SPI_FAMILY_VIT) {
+    run_gemm(head_, w.bufs[7], B, D_, out[0], classes_, true, Act::None, nullptr, false, 0, w.partial, s);
+  }
+}
+
+void Model::forward(hipStream_t s, int B, int S, size_t n, const void* const* in, void* const* out) {
+  if (device_ < 0) throw std::runtime_error("host-only replica (device < 0) cannot run a forward");
+  if (family_ == SPI_FAMILY_AFFINE) {
+    affine(static_cast<const float*>(in[0]), static_cast<float*>(out[0]), n, aff_scale_, aff_shift_, s);
+    return;
+  }
+  Workspace* w = workspace(s);
+  prologue(*w, B, S, in, s);
+  if (graphs_ && s != nullptr) {
+    const int key = (B * 2 + (w->has_mask ? 1 : 0)) * 4096 + S;
+    auto it = w->graphs.find(key);
+    if (it == w->graphs.end()) {
+      SPI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      body(*w, B, S, s);
+      hipGraph_t g = nullptr;
+      SPI_HIP(hipStreamEndCapture(s, &g));
+      hipGraphExec_t e = nullptr;
+      SPI_HIP(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
+      (void)hipGraphDestroy(g);
+      it = w->graphs.emplace(key, e).first;
+    }
+    SPI_HIP(hipGraphLaunch(it->second, s));
+  } else {
+    body(*w, B, S, s);
+  }
+  epilogue(*w, B, S, out, s);
+}
+
+}  // namespace spi
+
+namespace spi {
+
+void Model::op_begin(hipStream_t s, const std::string& name, double flops, double bytes) {
+  OpRecord r{name, flops, bytes, nullptr, nullptr};
+  SPI_HIP(hipEventCreate(&r.start));
+  SPI_HIP(hipEventCreate(&r.stop));
+  SPI_HIP(hipEventRecord(r.start, s));
+  prof_->push_back(r);
+}
+
+void Model::op_end(hipStream_t s) { SPI_HIP(hipEventRecord(prof_->back().stop, s)); }
+
+int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* const* out, float* ms,
+                   double* flops, double* bytes, char* names, int name_len, int max_ops) {
+  if (family_ == SPI_FAMILY_AFFINE) return 0;
+  if (device_ < 0) throw std::runtime_error("host-only replica (device < 0) cannot run a forward");
+  std::vector<OpRecord> recs;
+  Workspace* w = workspace(s);
+  prof_ = &recs;
+  try {
+    prologue(*w, B, S, in, s);
+    body(*w, B, S, s);
+    epilogue(*w, B, S, out, s);
+  } catch (...) {
+    prof_ = nullptr;
+    throw;
+  }
+  prof_ = nullptr;
+  SPI_HIP(hipStreamSynchronize(s));
+  int n = 0;
+  for (auto& r : recs) {
+    if (n < max_ops) {
+      float t = 0.f;
+      SPI_HIP(hipEventElapsedTime(&t, r.start, r.stop));
+      if (ms) ms[n] = t;
+      if (flops) flops[n] = r.flops;
+      if (bytes) bytes[n] = r.bytes;
+      if (names && name_len > 0) std::snprintf(names + (size_t)n * name_len, name_len, "%s", r.name.c_str());
+      ++n;
+    }
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
+  }
+  return n;
+}
+
+}  // namespace spi

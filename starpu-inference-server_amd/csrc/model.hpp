@@ -1,0 +1,151 @@
+// Device-resident model replica: the MI355X replacement for the per-device
+// TorchScript clones of inference_runner.cpp:251-275.  Weights are recognised
+// by their torchvision / HF parameter names, BN is folded into the convs, every
+// contraction weight is packed [Npad][Kpad] in the compute type, and the whole
+// replica lives in one HBM blob.  Activations live in per-stream workspaces
+// (one per StarPU worker stream: replicas are shared read-only by the workers
+// of a device, starpu_setup.cpp:725-778 / docs/server_guide.md:116).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/spi_codelet.h"
+#include "spi_kernels.hpp"
+
+namespace spi {
+
+struct ConvW {
+  size_t w = 0, b = 0;  // blob offsets (packed weight, fp32 bias)
+  int cout = 0, cin = 0, cin_pad = 0, kh = 1, kw = 1, stride = 1, pad = 0;
+  int kpad = 0, npad = 0;
+};
+
+struct LinearW {
+  size_t w = 0, b = 0;
+  int n = 0, k = 0, kpad = 0, npad = 0;
+  bool has_bias = true;
+};
+
+struct LnW {
+  size_t g = 0, b = 0;
+};
+
+struct ResBlock {
+  ConvW c1, c2, c3;  // c3 only for bottleneck
+  bool has_ds = false;
+  ConvW ds;
+};
+
+struct TfLayer {  // BERT (post-LN) / ViT (pre-LN) encoder layer
+  LinearW qkv, out, ff1, ff2;
+  LnW ln1, ln2;
+};
+
+struct Workspace;
+
+class Model {
+ public:
+  Model(int device, const spi_model_config& cfg, const spi_named_tensor* params, int n);
+  ~Model();
+
+  int device() const { return device_; }
+  int family() const { return family_; }
+  bool f16() const { return f16_; }
+  int max_batch() const { return max_batch_; }
+  size_t weight_bytes() const { return blob_bytes_; }
+  const std::string& describe() const { return desc_; }
+  double flops(int64_t batch) const;
+  void set_graphs(bool on) { graphs_ = on; }
+
+  // Validates the task's I/O against the replica; throws std::runtime_error
+  // with the reference's message wording on mismatch.
+  void check_io(const spi_codelet_args& a, const size_t* in_bytes,
+                const size_t* out_bytes) const;
+  // Enqueue the forward on `s`; never synchronises.
+  // S: BERT sequence length (ignored otherwise); n: AFFINE element count.
+  void forward(hipStream_t s, int batch, int S, size_t n, const void* const* in, void* const* out);
+
+  // Per-op profile of one forward: each launch bracketed by hipEvents on `s`.
+  struct OpRecord {
+    std::string name;
+    double flops;
+    double bytes;
+    hipEvent_t start, stop;
+  };
+  int profile(hipStream_t s, int batch, int S, const void* const* in, void* const* out, float* ms,
+              double* flops, double* bytes, char* names, int name_len, int max_ops);
+
+  // Output element count per sample (for size checks).
+  size_t out_elems_per_sample() const;
+  int num_inputs_min() const;
+  int num_inputs_max() const;
+
+ private:
+  void build_resnet(const std::map<std::string, const spi_named_tensor*>& p);
+  void build_bert(const std::map<std::string, const spi_named_tensor*>& p);
+  void build_vit(const std::map<std::string, const spi_named_tensor*>& p);
+  Workspace* workspace(hipStream_t s);
+  void body(Workspace& w, int batch, int S, hipStream_t s);
+  void prologue(Workspace& w, int batch, int S, const void* const* in, hipStream_t s);
+  void epilogue(Workspace& w, int batch, int S, void* const* out, hipStream_t s);
+  void run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc,
+                bool out_f32, Act act, const void* res, bool res_f32, int ldr, float* partial,
+                hipStream_t s);
+  void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
+                Act act, const void* res, float* partial, hipStream_t s);
+  size_t conv_partial(const ConvW& c, int B, int H, int W) const;
+  size_t linear_partial(const LinearW& L, int M) const;
+  template <typename P>
+  const P* ptr(size_t off) const {
+    return reinterpret_cast<const P*>(static_cast<const char*>(dblob_) + off);
+  }
+
+  int device_ = 0;
+  int family_ = 0;
+  bool f16_ = true;
+  int max_batch_ = 1;
+  bool graphs_ = false;
+  std::string desc_;
+  std::vector<char> hblob_;
+  void* dblob_ = nullptr;
+  size_t blob_bytes_ = 0;
+
+  // AFFINE
+  float aff_scale_ = 1.f, aff_shift_ = 0.f;
+  // ResNet
+  bool bottleneck_ = false;
+  std::vector<int> stage_blocks_;
+  ConvW stem_;
+  std::vector<ResBlock> blocks_;
+  LinearW fc_;
+  int image_ = 224, classes_ = 1000, feat_ = 512;
+  // transformers
+  int D_ = 768, heads_ = 12, ffn_ = 3072, seq_ = 128, layers_ = 0, vocab_ = 0, maxpos_ = 0;
+  float eps_ = 1e-12f;
+  size_t word_ = 0, pos_ = 0, type0_ = 0;
+  LnW emb_ln_, final_ln_;
+  std::vector<TfLayer> tf_;
+  // ViT
+  int patch_ = 16, npatch_ = 196;
+  LinearW patch_proj_, head_;
+  size_t cls_ = 0, vpos_ = 0;
+
+  std::mutex mu_;
+  std::map<hipStream_t, std::unique_ptr<Workspace>> ws_;
+  std::vector<OpRecord>* prof_ = nullptr;  // set only inside profile()
+  void op_begin(hipStream_t s, const std::string& name, double flops, double bytes);
+  void op_end(hipStream_t s);
+
+  friend struct Workspace;
+};
+
+}  // namespace spi
+
+struct spi_model {
+  std::unique_ptr<spi::Model> impl;
+};

@@ -1,0 +1,86 @@
+// Internal launch interface of the HIP/CDNA4 kernels (gfx950 only).
+// Every launcher enqueues on the given stream and never synchronises, so a
+// forward pass can be captured into a hipGraph (cdna_hip_programming.md G9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <cstdint>
+
+namespace spi {
+
+enum class Act : int { None = 0, Relu = 1, Gelu = 2 };
+
+// C[M,N] = act(A[M,K] . W[N,K]^T + bias[N] + residual[M,N])
+//
+// A is either a dense row-major activation (lda) or, for conv-as-implicit-GEMM,
+// an NHWC image gathered on the fly: row m = (img, oh, ow), column
+// k = (kh*KW + kw)*Cin + c.  W is pre-packed [Npad][Kpad] (K contiguous,
+// zero padded), so both MFMA operands are K-contiguous 16-byte chunks.
+struct GemmDesc {
+  int M = 0, N = 0, K = 0;  // logical sizes
+  int Kpad = 0;             // W row stride (multiple of 64)
+  int lda = 0;              // dense A row stride (elements)
+  int ldc = 0;              // C row stride (elements)
+  int ldr = 0;              // residual row stride (elements)
+  // conv geometry (conv == true)
+  bool conv = false;
+  int H = 0, W = 0, Cin = 0, OH = 0, OW = 0, KH = 1, KW = 1, stride = 1, pad = 0;
+  Act act = Act::None;
+  bool out_f32 = false;  // C is float (else the compute type)
+  bool res_f32 = false;  // residual is float (else the compute type)
+};
+
+struct GemmPtrs {
+  const void* A = nullptr;
+  const void* W = nullptr;
+  const float* bias = nullptr;
+  const void* res = nullptr;
+  void* C = nullptr;
+  float* partial = nullptr;  // split-K workspace: splits * M * N floats
+};
+
+// Workspace floats needed by a GEMM with the chosen split-K.
+size_t gemm_partial_floats(const GemmDesc& d, bool f16);
+void gemm(const GemmDesc& d, const GemmPtrs& p, bool f16, hipStream_t s);
+
+// NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
+void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
+                 bool f16, hipStream_t s);
+// 3x3/s2/p1 max pool on NHWC.
+void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH,
+                  int OW, int k, int stride, int pad, bool f16, hipStream_t s);
+// Global average pool NHWC [B,HW,C] -> [B,C] (compute type).
+void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16,
+                  hipStream_t s);
+// Row LayerNorm over D: y = LN(x) * g + b.  x fp32 [rows, ldx]; writes fp32
+// (yf, may alias x) and/or compute-type (yt) outputs.
+void layernorm(const float* x, int ldx, const float* g, const float* b,
+               float* yf, void* yt, int ldy, int rows, int D, float eps, bool f16,
+               hipStream_t s);
+// BERT embeddings: LN(word[ids] + pos[s] + type[0]) -> fp32 + compute type.
+void bert_embed(const int64_t* ids, const float* word, const float* pos,
+                const float* type0, const float* g, const float* b, float* yf,
+                void* yt, int B, int S, int D, int vocab, float eps, bool f16,
+                hipStream_t s);
+// int64 attention mask [B,S] -> additive fp32 bias [B,S] (0 or finfo.min).
+void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s);
+// ViT: NCHW fp32 image -> patch rows [B*P, C*ps*ps] (compute type).
+void patchify(const float* x, void* y, int B, int C, int H, int W, int ps,
+              bool f16, hipStream_t s);
+// ViT: x[b, 0] = cls + pos[0]; x[b, 1+p] = patch[b, p] + pos[1+p]  (fp32).
+void vit_assemble(const float* patches, const float* cls, const float* pos,
+                  float* x, int B, int P, int D, hipStream_t s);
+// Gather rows: y[i] = x[i * stride_rows] (fp32 -> compute type) for CLS pooling.
+void gather_rows(const float* x, void* y, int rows, int stride_rows, int D,
+                 bool f16, hipStream_t s);
+// y = x * scale + shift, fp32 elementwise (AFFINE toy family).
+void affine(const float* x, float* y, size_t n, float scale, float shift,
+            hipStream_t s);
+
+// Multi-head attention over a packed qkv buffer [B*S, 3*D] (compute type):
+// ctx[b*S+i, h*hd:(h+1)*hd] = softmax(q k^T * scale + mask_bias[b]) v.
+// mask_bias: fp32 [B, S] additive bias or nullptr.
+void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S,
+               int heads, int hd, float scale, bool f16, hipStream_t s);
+
+}  // namespace spi

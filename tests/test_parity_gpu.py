@@ -1,0 +1,144 @@
+"""GPU parity: the HIP codelet (through the C-ABI) vs the CPU codelet oracle.
+
+Metric: normalised max-abs error max|hip - ref| / max|ref| plus top-1
+agreement for classifiers (hard part 3).  Tolerances
+(BASELINE.json north_star): fp32 1e-5; fp16 compute (fp16 MFMA operands, fp32
+accumulation, fp32 residual stream / LN / softmax) 1e-3 for the model families
+at the reference configs.  Inputs are seeded synthetic data shaped like the
+reference's input generator (src/utils/input_generator.hpp:22-88).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_codelet import cpu_inference, normalized_max_error, top1_agreement
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": 1e-5, "fp16": 1e-3}
+
+
+def hip_forward(spi, replica, inputs, out_shape, graphs=False):
+    ins = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in inputs]
+    out = torch.full(out_shape, float("nan"), device="cuda", dtype=torch.float32)
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    replica.set_graphs(graphs)
+    spi.run_hip(replica, ins, out, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def image(rng, b, size):
+    return rng.random((b, 3, size, size), dtype=np.float32)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_resnet18_small_image(spi, zoo, gpu, prec):
+    rng = np.random.default_rng(0)
+    m = zoo.resnet18(image=64)
+    x = image(rng, 3, 64)
+    ref = cpu_inference(m, [x])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=4, image_size=64)
+    got = hip_forward(spi, rep, [x], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@64 {prec} err={err:.3e}")
+    assert np.isfinite(got).all()
+    assert err < TOL[prec] * 2
+    assert top1_agreement(got, ref) == 1.0
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_resnet_bottleneck_small(spi, zoo, gpu, prec):
+    rng = np.random.default_rng(1)
+    m = zoo.resnet([1, 2, 2, 1], True, image=64)
+    x = image(rng, 2, 64)
+    ref = cpu_inference(m, [x])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=2, image_size=64)
+    got = hip_forward(spi, rep, [x], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"resnet-bottleneck@64 {prec} err={err:.3e}")
+    assert err < TOL[prec] * 2
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_resnet18_full_bs8(spi, zoo, gpu, prec):
+    """C2: ResNet-18 bs=8 at 224x224."""
+    rng = np.random.default_rng(2)
+    m = zoo.resnet18()
+    x = image(rng, 8, 224)
+    ref = cpu_inference(m, [x])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=8)
+    got = hip_forward(spi, rep, [x], ref.shape)
+    got_g = hip_forward(spi, rep, [x], ref.shape, graphs=True)
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@224 bs8 {prec} err={err:.3e}")
+    assert err < TOL[prec]
+    assert top1_agreement(got, ref) == 1.0
+    np.testing.assert_array_equal(got, got_g)
+
+
+def bert_inputs(rng, b, s, vocab=30522, pad_from=None):
+    ids = rng.integers(0, vocab, size=(b, s), dtype=np.int64)
+    mask = np.ones((b, s), dtype=np.int64)
+    if pad_from is not None:
+        mask[-1, pad_from:] = 0
+    return ids, mask
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_bert_two_layers_masked(spi, zoo, gpu, prec):
+    rng = np.random.default_rng(3)
+    m = zoo.bert(layers=2, init_std=0.05)
+    ids, mask = bert_inputs(rng, 3, 80, pad_from=50)
+    ref = cpu_inference(m, [ids, mask])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=3, seq_len=128)
+    got = hip_forward(spi, rep, [ids, mask], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"bert L2 S80 masked {prec} err={err:.3e}")
+    assert err < TOL[prec] * 2
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_bert_base_seq128_bs8(spi, zoo, gpu, prec):
+    """C3: bert-base-uncased seq=128 bs=8 (mask all ones)."""
+    rng = np.random.default_rng(4)
+    m = zoo.bert_base()
+    ids, mask = bert_inputs(rng, 8, 128)
+    ref = cpu_inference(m, [ids, mask])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=8, seq_len=128)
+    got = hip_forward(spi, rep, [ids, mask], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"bert-base S128 bs8 {prec} err={err:.3e}")
+    assert err < TOL[prec]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_vit_small_seq197(spi, zoo, gpu, prec):
+    """ViT at 224/16 (S=197: three full 64-key tiles + a 5-key tail), small width."""
+    rng = np.random.default_rng(5)
+    m = zoo.vit(image=224, patch=16, layers=2, heads=2, dim=128, mlp_dim=256)
+    x = image(rng, 2, 224)
+    ref = cpu_inference(m, [x])[0]
+    rep = spi.ModelReplica(m, 0, prec, max_batch=2)
+    got = hip_forward(spi, rep, [x], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"vit-small S197 {prec} err={err:.3e}")
+    assert err < TOL[prec] * 2
+
+
+def test_affine_codelet_like_reference(spi, gpu):
+    """x + 1.5 on {1,2,3} (tests/unit/core/unit_starpu_setup.cpp:2332-2433)."""
+    rep = spi.ModelReplica(None, 0, "fp32", max_batch=3, family="affine", affine=(1.0, 1.5))
+    x = torch.tensor([1.0, 2.0, 3.0], device="cuda")
+    out = torch.zeros(3, device="cuda")
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    params = spi.make_params([[3]], [torch.float32], models_gpu=[rep])
+    bufs = [spi.make_variable_interface(x.data_ptr(), 12), spi.make_variable_interface(out.data_ptr(), 12)]
+    with spi.worker_context(77, 0, stream.cuda_stream):
+        args = spi.InferenceCodelet.hip_inference_func(bufs, params)
+    stream.synchronize()
+    assert out.cpu().tolist() == [2.5, 3.5, 4.5]
+    assert args.device_id == 0 and args.worker_id == 77 and args.executed_on == 2
+    assert args.codelet_start_ns > 0 and args.codelet_end_ns >= args.codelet_start_ns
