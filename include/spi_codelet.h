@@ -229,7 +229,10 @@ enum spi_family {
   SPI_FAMILY_AFFINE = 4  /* y = x * scale + shift (toy models of the reference tests) */
 };
 
-enum spi_precision { SPI_PREC_F32 = 0, SPI_PREC_F16 = 1 };
+/* SPI_PREC_F16X3: split fp16 -- fp32 activations, each MFMA operand split into
+ * hi + lo fp16 halves, hi*hi + hi*lo + lo*hi per fragment (fp32-grade
+ * results at the fp16 MFMA rate). */
+enum spi_precision { SPI_PREC_F32 = 0, SPI_PREC_F16 = 1, SPI_PREC_F16X3 = 2 };
 
 typedef struct spi_named_tensor {
   const char* name; /* parameter/buffer name as in named_parameters() */

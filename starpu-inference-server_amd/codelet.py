@@ -124,6 +124,8 @@ def load_model(path: str) -> torch.jit.ScriptModule:
     return m
 
 
+PRECISIONS = {"fp16": N.PREC_F16, "f16": N.PREC_F16, "fp32": N.PREC_F32, "f32": N.PREC_F32,
+              "fp16x3": N.PREC_F16X3, "f16x3": N.PREC_F16X3}
 _FAMILIES = {None: N.FAMILY_AUTO, "auto": N.FAMILY_AUTO, "resnet": N.FAMILY_RESNET, "bert": N.FAMILY_BERT,
              "vit": N.FAMILY_VIT, "affine": N.FAMILY_AFFINE}
 
@@ -152,7 +154,7 @@ class ModelReplica:
                 arr[i].shape[d] = s
         cfg = N.ModelConfig()
         cfg.family = _FAMILIES[family]
-        cfg.precision = {"fp16": N.PREC_F16, "f16": N.PREC_F16, "fp32": N.PREC_F32, "f32": N.PREC_F32}[precision]
+        cfg.precision = PRECISIONS[precision]
         cfg.max_batch = max_batch
         cfg.num_heads = num_heads
         cfg.seq_len = seq_len

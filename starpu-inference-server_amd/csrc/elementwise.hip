@@ -36,45 +36,91 @@ __global__ void ingest_kernel(const float* __restrict__ x, T* __restrict__ y, in
   }
 }
 
-// Max pool on NHWC; thread per (pixel, channel).
+// Max pool on NHWC; one thread per (output pixel, 16-byte channel vector).
 template <typename T>
 __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
                                int W, int C, int OH, int OW, int k, int stride, int pad) {
-  const size_t n = (size_t)B * OH * OW * C;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  const int CV = C / VEC;
+  const size_t n = (size_t)B * OH * OW * CV;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    size_t r = i / C;
+    const int cv = (int)(i % CV);
+    size_t r = i / CV;
     const int ow = (int)(r % OW);
     r /= OW;
     const int oh = (int)(r % OH);
     const int b = (int)(r / OH);
-    float m = -INFINITY;
+    float m[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) m[e] = -INFINITY;
     for (int kh = 0; kh < k; ++kh) {
       const int ih = oh * stride - pad + kh;
       if ((unsigned)ih >= (unsigned)H) continue;
       for (int kw = 0; kw < k; ++kw) {
         const int iw = ow * stride - pad + kw;
         if ((unsigned)iw >= (unsigned)W) continue;
-        m = fmaxf(m, static_cast<float>(x[(((size_t)b * H + ih) * W + iw) * C + c]));
+        const uint4 v = *reinterpret_cast<const uint4*>(x + (((size_t)b * H + ih) * W + iw) * C + cv * VEC);
+        const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) m[q] = fmaxf(m[q], static_cast<float>(e[q]));
       }
     }
-    y[i] = cvt<T>(m);
+    T o[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) o[q] = cvt<T>(m[q]);
+    *reinterpret_cast<uint4*>(y + i * VEC) = *reinterpret_cast<const uint4*>(o);
   }
 }
 
-// Global average pool: thread per (b, c), sums HW in fp32.
+// Global average pool: one block per image; thread (g, c) sums pixels g, g+G, ...
+// of its 16-byte channel vector c, then the G partial sums meet in LDS.
 template <typename T>
-__global__ void avgpool_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int HW,
-                               int C) {
-  const size_t n = (size_t)B * C;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x) {
-    const size_t b = i / C, c = i - b * C;
-    const T* p = x + b * HW * C + c;
-    float s = 0.f;
-    for (int j = 0; j < HW; ++j) s += static_cast<float>(p[(size_t)j * C]);
-    y[i] = cvt<T>(s / (float)HW);
+__global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                      int B, int HW, int C) {
+  constexpr int VEC = 16 / (int)sizeof(T);
+  __shared__ float part[256 * VEC];
+  const int b = blockIdx.x;
+  const int CV = C / VEC;
+  const T* img = x + (size_t)b * HW * C;
+  if (CV <= 256) {
+    const int G = 256 / CV;
+    const int g = threadIdx.x / CV, cv = threadIdx.x % CV;
+    float s[VEC] = {};
+    if (g < G)
+      for (int p = g; p < HW; p += G) {
+        const uint4 v = *reinterpret_cast<const uint4*>(img + (size_t)p * C + cv * VEC);
+        const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) s[q] += static_cast<float>(e[q]);
+      }
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) part[threadIdx.x * VEC + q] = s[q];
+    __syncthreads();
+    if (threadIdx.x < CV) {
+      T o[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        float t = 0.f;
+        for (int gg = 0; gg < G; ++gg) t += part[(gg * CV + threadIdx.x) * VEC + q];
+        o[q] = cvt<T>(t / (float)HW);
+      }
+      *reinterpret_cast<uint4*>(y + (size_t)b * C + threadIdx.x * VEC) = *reinterpret_cast<const uint4*>(o);
+    }
+  } else {
+    for (int cv = threadIdx.x; cv < CV; cv += 256) {
+      float s[VEC] = {};
+      for (int p = 0; p < HW; ++p) {
+        const uint4 v = *reinterpret_cast<const uint4*>(img + (size_t)p * C + cv * VEC);
+        const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) s[q] += static_cast<float>(e[q]);
+      }
+      T o[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o[q] = cvt<T>(s[q] / (float)HW);
+      *reinterpret_cast<uint4*>(y + (size_t)b * C + cv * VEC) = *reinterpret_cast<const uint4*>(o);
+    }
   }
 }
 
@@ -226,7 +272,7 @@ void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad, 
 
 void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH, int OW, int k,
                   int stride, int pad, bool f16, hipStream_t s) {
-  const size_t n = (size_t)B * OH * OW * C;
+  const size_t n = (size_t)B * OH * OW * C / (f16 ? 8 : 4);
   if (f16)
     hipLaunchKernelGGL((maxpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
                        (const _Float16*)x, (_Float16*)y, B, H, W, C, OH, OW, k, stride, pad);
@@ -236,13 +282,12 @@ void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH, in
 }
 
 void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s) {
-  const size_t n = (size_t)B * C;
   if (f16)
-    hipLaunchKernelGGL((avgpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
-                       (const _Float16*)x, (_Float16*)y, B, HW, C);
+    hipLaunchKernelGGL((avgpool_kernel<_Float16>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
+                       (_Float16*)y, B, HW, C);
   else
-    hipLaunchKernelGGL((avgpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
-                       (const float*)x, (float*)y, B, HW, C);
+    hipLaunchKernelGGL((avgpool_kernel<float>), dim3(B), dim3(256), 0, s, (const float*)x,
+                       (float*)y, B, HW, C);
 }
 
 void layernorm(const float* x, int ldx, const float* g, const float* b, float* yf, void* yt,

@@ -52,6 +52,8 @@ int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 }  // namespace
 
+constexpr size_t kCounterSlots = 16384;  // >= tiles of any split GEMM (checked per launch)
+
 // ---------------------------------------------------------------------------
 // Workspace: activation buffers for one stream at max_batch.
 // ---------------------------------------------------------------------------
@@ -59,6 +61,8 @@ struct Workspace {
   std::vector<void*> bufs;
   float* partial = nullptr;
   float* mask_bias = nullptr;
+  size_t partial_floats = 0;
+  int* counters = nullptr;  // split-K tickets (zeroed once; the reducer re-zeroes its slot)
   bool has_mask = false;
   std::map<int, hipGraphExec_t> graphs;
   ~Workspace() {
@@ -66,6 +70,7 @@ struct Workspace {
     for (void* b : bufs) (void)hipFree(b);
     if (partial) (void)hipFree(partial);
     if (mask_bias) (void)hipFree(mask_bias);
+    if (counters) (void)hipFree(counters);
   }
 };
 
@@ -91,18 +96,24 @@ Blob* g_blob = nullptr;  // only used during construction (single thread)
 // Pack a [N][K] fp32 matrix (row-major, K contiguous) into [Npad][Kpad] of the
 // compute type.  get(n, k) supplies element (n, k) in packed-k order.
 template <typename F>
-size_t pack_matrix(int N, int K, int Npad, int Kpad, bool f16, F get) {
-  const size_t es = f16 ? 2 : 4;
-  const size_t off = g_blob->add(nullptr, (size_t)Npad * Kpad * es);
+size_t pack_matrix(int N, int K, int Npad, int Kpad, Prec prec, F get) {
+  const size_t plane = (size_t)Npad * Kpad;
+  const size_t bytes = prec == Prec::F32 ? plane * 4 : prec == Prec::F16 ? plane * 2 : plane * 4;
+  const size_t off = g_blob->add(nullptr, bytes);
   char* dst = g_blob->at(off);
-  std::memset(dst, 0, (size_t)Npad * Kpad * es);
+  std::memset(dst, 0, bytes);
   for (int n = 0; n < N; ++n)
     for (int k = 0; k < K; ++k) {
       const float v = get(n, k);
-      if (f16)
-        reinterpret_cast<_Float16*>(dst)[(size_t)n * Kpad + k] = static_cast<_Float16>(v);
-      else
-        reinterpret_cast<float*>(dst)[(size_t)n * Kpad + k] = v;
+      const size_t i = (size_t)n * Kpad + k;
+      if (prec == Prec::F32) {
+        reinterpret_cast<float*>(dst)[i] = v;
+      } else {
+        const _Float16 hi = static_cast<_Float16>(v);
+        reinterpret_cast<_Float16*>(dst)[i] = hi;
+        if (prec == Prec::F16X3)  // lo plane: the residual fp16 cannot hold
+          reinterpret_cast<_Float16*>(dst)[plane + i] = static_cast<_Float16>(v - static_cast<float>(hi));
+      }
     }
   return off;
 }
@@ -112,7 +123,7 @@ size_t pack_vec(const float* v, int n) { return g_blob->add(v, (size_t)n * sizeo
 // Conv weight [Cout][Cin][KH][KW] (+ eval BN) -> folded [Npad][Kpad], k =
 // (kh*KW + kw)*cin_pad + c; bias' = beta - mean * gamma / sqrt(var + eps).
 ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
-                int cin_pad, bool f16, float bn_eps) {
+                int cin_pad, Prec prec, float bn_eps) {
   const spi_named_tensor* wt = need(p, wname + ".weight");
   if (wt->ndim != 4) throw std::runtime_error(wname + ".weight must be 4-D");
   ConvW c;
@@ -143,7 +154,8 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   }
   const float* w = fdata(wt);
   const int cin = c.cin, kh = c.kh, kw = c.kw, cp = c.cin_pad;
-  c.w = pack_matrix(c.cout, K, c.npad, c.kpad, f16, [&](int n, int k) -> float {
+  c.wplane = (size_t)c.npad * c.kpad;
+  c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, [&](int n, int k) -> float {
     const int cell = k / cp, ci = k % cp;
     if (ci >= cin) return 0.f;
     const int y = cell / kw, x = cell % kw;
@@ -155,13 +167,14 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   return c;
 }
 
-LinearW pack_linear(const float* w, const float* b, int N, int K, bool f16) {
+LinearW pack_linear(const float* w, const float* b, int N, int K, Prec prec) {
   LinearW L;
   L.n = N;
   L.k = K;
   L.kpad = round_up(K, 64);
   L.npad = round_up(N, 128);
-  L.w = pack_matrix(N, K, L.npad, L.kpad, f16,
+  L.wplane = (size_t)L.npad * L.kpad;
+  L.w = pack_matrix(N, K, L.npad, L.kpad, prec,
                     [&](int n, int k) { return w[(size_t)n * K + k]; });
   std::vector<float> zeros;
   if (!b) {
@@ -173,11 +186,11 @@ LinearW pack_linear(const float* w, const float* b, int N, int K, bool f16) {
   return L;
 }
 
-LinearW pack_linear_named(const PMap& p, const std::string& name, bool f16) {
+LinearW pack_linear_named(const PMap& p, const std::string& name, Prec prec) {
   const spi_named_tensor* wt = need(p, name + ".weight");
   if (wt->ndim != 2) throw std::runtime_error(name + ".weight must be 2-D");
   const float* b = has(p, name + ".bias") ? fdata(need(p, name + ".bias")) : nullptr;
-  return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], f16);
+  return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], prec);
 }
 
 LnW pack_ln(const PMap& p, const std::string& name) {
@@ -226,9 +239,10 @@ bool ends_with(const PMap& p, const std::string& anchor) {
 // Construction
 // ---------------------------------------------------------------------------
 Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* params, int n)
-    : device_(device), family_(cfg.family), f16_(cfg.precision == SPI_PREC_F16),
+    : device_(device), family_(cfg.family), prec_(cfg.precision == SPI_PREC_F16 ? Prec::F16 : cfg.precision == SPI_PREC_F16X3 ? Prec::F16X3 : Prec::F32),
+      f16_(cfg.precision == SPI_PREC_F16),
       max_batch_(std::max(1, cfg.max_batch)) {
-  if (cfg.precision != SPI_PREC_F16 && cfg.precision != SPI_PREC_F32)
+  if (cfg.precision != SPI_PREC_F16 && cfg.precision != SPI_PREC_F32 && cfg.precision != SPI_PREC_F16X3)
     throw std::runtime_error("unsupported precision");
   PMap p;
   for (int i = 0; i < n; ++i) {
@@ -271,7 +285,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
   } else {
     throw std::runtime_error("unsupported model family");
   }
-  os << (f16_ ? " f16" : " f32") << " maxB" << max_batch_;
+  os << (prec_ == Prec::F16 ? " f16" : prec_ == Prec::F16X3 ? " f16x3" : " f32") << " maxB" << max_batch_;
   desc_ = os.str();
   g_blob = nullptr;
 
@@ -293,8 +307,8 @@ void Model::build_resnet(const PMap& p) {
   // Stages: torchvision layer1..layer4, stride 2 on the first block of 2..4
   // (on conv1 for BasicBlock, conv2 for Bottleneck: torchvision v1.5).
   bottleneck_ = has(p, "layer1.0.conv3.weight");
-  const int cin_pad = f16_ ? 8 : 4;
-  stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, f16_, eps_);
+  const int cin_pad = prec_ == Prec::F32 ? 4 : 8;
+  stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, prec_, eps_);
   if (stem_.kh != 7 || stem_.cin != 3) throw std::runtime_error("resnet stem must be 7x7 over 3 channels");
   for (int L = 1; L <= 4; ++L) {
     int nb = 0;
@@ -306,19 +320,19 @@ void Model::build_resnet(const PMap& p) {
       const int s = (L > 1 && i == 0) ? 2 : 1;
       ResBlock blk;
       if (bottleneck_) {
-        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", 1, 0, f16_, eps_);
-        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", s, 0, f16_, eps_);
-        blk.c3 = pack_conv(p, pre + "conv3", pre + "bn3", 1, 0, f16_, eps_);
+        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", 1, 0, prec_, eps_);
+        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", s, 0, prec_, eps_);
+        blk.c3 = pack_conv(p, pre + "conv3", pre + "bn3", 1, 0, prec_, eps_);
       } else {
-        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", s, 0, f16_, eps_);
-        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", 1, 0, f16_, eps_);
+        blk.c1 = pack_conv(p, pre + "conv1", pre + "bn1", s, 0, prec_, eps_);
+        blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", 1, 0, prec_, eps_);
       }
       blk.has_ds = has(p, pre + "downsample.0.weight");
-      if (blk.has_ds) blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, f16_, eps_);
+      if (blk.has_ds) blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_);
       blocks_.push_back(blk);
     }
   }
-  fc_ = pack_linear_named(p, "fc", f16_);
+  fc_ = pack_linear_named(p, "fc", prec_);
   classes_ = fc_.n;
   feat_ = fc_.k;
   for (auto& b : blocks_) {
@@ -357,11 +371,11 @@ void Model::build_bert(const PMap& p) {
       std::memcpy(w.data() + (size_t)j * D_ * D_, fdata(need(p, nm + ".weight")), sizeof(float) * D_ * D_);
       std::memcpy(b.data() + (size_t)j * D_, fdata(need(p, nm + ".bias")), sizeof(float) * D_);
     }
-    L.qkv = pack_linear(w.data(), b.data(), 3 * D_, D_, f16_);
-    L.out = pack_linear_named(p, pre + "attention.output.dense", f16_);
+    L.qkv = pack_linear(w.data(), b.data(), 3 * D_, D_, prec_);
+    L.out = pack_linear_named(p, pre + "attention.output.dense", prec_);
     L.ln1 = pack_ln(p, pre + "attention.output.LayerNorm");
-    L.ff1 = pack_linear_named(p, pre + "intermediate.dense", f16_);
-    L.ff2 = pack_linear_named(p, pre + "output.dense", f16_);
+    L.ff1 = pack_linear_named(p, pre + "intermediate.dense", prec_);
+    L.ff2 = pack_linear_named(p, pre + "output.dense", prec_);
     L.ln2 = pack_ln(p, pre + "output.LayerNorm");
     ffn_ = L.ff1.n;
     tf_.push_back(L);
@@ -380,7 +394,7 @@ void Model::build_vit(const PMap& p) {
   if (D_ % 64 != 0 || D_ > 1024) throw std::runtime_error("hidden size must be a multiple of 64, <= 1024");
   const int K = 3 * patch_ * patch_;
   patch_proj_ = pack_linear(fdata(cw), has(p, "conv_proj.bias") ? fdata(need(p, "conv_proj.bias")) : nullptr,
-                            D_, K, f16_);
+                            D_, K, prec_);
   cls_ = pack_vec(fdata(need(p, "class_token")), D_);
   const spi_named_tensor* pe = need(p, "encoder.pos_embedding");
   if (numel(pe) != (int64_t)(npatch_ + 1) * D_) throw std::runtime_error("pos_embedding does not match image/patch size");
@@ -393,18 +407,18 @@ void Model::build_vit(const PMap& p) {
     L.ln1 = pack_ln(p, pre + "ln_1");
     const spi_named_tensor* iw = need(p, pre + "self_attention.in_proj_weight");
     L.qkv = pack_linear(fdata(iw), fdata(need(p, pre + "self_attention.in_proj_bias")), (int)iw->shape[0],
-                        (int)iw->shape[1], f16_);
-    L.out = pack_linear_named(p, pre + "self_attention.out_proj", f16_);
+                        (int)iw->shape[1], prec_);
+    L.out = pack_linear_named(p, pre + "self_attention.out_proj", prec_);
     L.ln2 = pack_ln(p, pre + "ln_2");
     const std::string m1 = has(p, pre + "mlp.0.weight") ? pre + "mlp.0" : pre + "mlp.linear_1";
     const std::string m2 = has(p, pre + "mlp.3.weight") ? pre + "mlp.3" : pre + "mlp.linear_2";
-    L.ff1 = pack_linear_named(p, m1, f16_);
-    L.ff2 = pack_linear_named(p, m2, f16_);
+    L.ff1 = pack_linear_named(p, m1, prec_);
+    L.ff2 = pack_linear_named(p, m2, prec_);
     ffn_ = L.ff1.n;
     tf_.push_back(L);
   }
   final_ln_ = pack_ln(p, "encoder.ln");
-  head_ = pack_linear_named(p, "heads.head", f16_);
+  head_ = pack_linear_named(p, "heads.head", prec_);
   classes_ = head_.n;
   seq_ = npatch_ + 1;
 }
@@ -548,17 +562,18 @@ GemmDesc linear_desc(const LinearW& L, int M, int lda, int ldc) {
 
 size_t Model::conv_partial(const ConvW& c, int B, int H, int W) const {
   int OH, OW;
-  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW), f16_);
+  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW));
 }
 
 size_t Model::linear_partial(const LinearW& L, int M) const {
-  return gemm_partial_floats(linear_desc(L, M, L.k, L.n), f16_);
+  return gemm_partial_floats(linear_desc(L, M, L.k, L.n));
 }
 
 void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
-                     Act act, const void* res, float* partial, hipStream_t s) {
+                     Act act, const void* res, Workspace& ws, hipStream_t s) {
   GemmDesc d = conv_desc(c, B, H, W, OH, OW);
   d.act = act;
+  d.wplane = c.wplane;
   const size_t es = f16_ ? 2 : 4;
   if (prof_)
     op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
@@ -571,18 +586,22 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   p.bias = ptr<float>(c.b);
   p.res = res;
   p.C = y;
-  p.partial = partial;
-  gemm(d, p, f16_, s);
+  p.partial = ws.partial;
+  p.counters = ws.counters;
+  if (gemm_partial_floats(d) > ws.partial_floats || gemm_counter_slots(d) > kCounterSlots)
+    throw std::runtime_error("split-K workspace too small");
+  gemm(d, p, prec_, s);
   if (prof_) op_end(s);
 }
 
 void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc, bool out_f32, Act act,
-                     const void* res, bool res_f32, int ldr, float* partial, hipStream_t s) {
+                     const void* res, bool res_f32, int ldr, Workspace& ws, hipStream_t s) {
   GemmDesc d = linear_desc(L, M, lda, ldc);
   d.act = act;
   d.out_f32 = out_f32;
   d.res_f32 = res_f32;
   d.ldr = ldr;
+  d.wplane = L.wplane;
   const size_t es = f16_ ? 2 : 4;
   if (prof_)
     op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
@@ -595,8 +614,11 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   p.bias = ptr<float>(L.b);
   p.res = res;
   p.C = C;
-  p.partial = partial;
-  gemm(d, p, f16_, s);
+  p.partial = ws.partial;
+  p.counters = ws.counters;
+  if (gemm_partial_floats(d) > ws.partial_floats || gemm_counter_slots(d) > kCounterSlots)
+    throw std::runtime_error("split-K workspace too small");
+  gemm(d, p, prec_, s);
   if (prof_) op_end(s);
 }
 
@@ -675,7 +697,13 @@ Workspace* Model::workspace(hipStream_t s) {
     SPI_HIP(hipMalloc(&b, std::max<size_t>(bytes, 256)));
     w->bufs.push_back(b);
   }
-  if (partial) SPI_HIP(hipMalloc(&w->partial, partial * sizeof(float)));
+  // Split-K slabs: choose_plan only splits grids of < 128 tiles into <= 512 +
+  // tiles workgroups of 64x64, so 640 * 64 * 64 floats bounds every batch size.
+  partial = std::max(partial, (size_t)640 * 64 * 64);
+  w->partial_floats = partial;
+  SPI_HIP(hipMalloc(&w->partial, partial * sizeof(float)));
+  SPI_HIP(hipMalloc(&w->counters, kCounterSlots * sizeof(int)));
+  SPI_HIP(hipMemset(w->counters, 0, kCounterSlots * sizeof(int)));
   Workspace* raw = w.get();
   ws_[s] = std::move(w);
   return raw;
@@ -687,7 +715,9 @@ Workspace* Model::workspace(hipStream_t s) {
 // ---------------------------------------------------------------------------
 void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
+    if (prof_) op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);
     ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
+    if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     bert_embed(static_cast<const int64_t*>(in[0]), ptr<float>(word_), ptr<float>(pos_), ptr<float>(type0_),
                ptr<float>(emb_ln_.g), ptr<float>(emb_ln_.b), static_cast<float*>(w.bufs[0]),
@@ -703,10 +733,12 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
     int H = image_, OH, OW;
     void* const* buf = w.bufs.data();
-    run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w.partial, s);
+    run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w, s);
     H = OH;
     const int PH = (H + 2 - 3) / 2 + 1;
+    if (prof_) op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
     maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    if (prof_) op_end(s);
     H = PH;
     int cur = 2;
     auto pick = [&](std::initializer_list<int> busy) {
@@ -718,32 +750,34 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       int H2;
       if (bottleneck_) {
         const int t1 = pick({cur});
-        run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w.partial, s);
+        run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w, s);
         const int t2 = pick({cur, t1});
-        run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w.partial, s);
+        run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
         if (b.has_ds) {
           ident = pick({cur, t2});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w.partial, s);
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
         }
         const int o = pick({cur, t2, ident});
-        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w.partial, s);
+        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
         cur = o;
       } else {
         const int t1 = pick({cur});
-        run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w.partial, s);
+        run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
         if (b.has_ds) {
           ident = pick({cur, t1});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w.partial, s);
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
         }
         const int o = pick({cur, t1, ident});
-        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w.partial, s);
+        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
         cur = o;
       }
       H = H2;
     }
+    if (prof_) op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
     avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+    if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const int S = S_in, T = B * S;
     float* hf = static_cast<float*>(w.bufs[0]);
@@ -755,14 +789,14 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     for (int i = 0; i < layers_; ++i) {
       const TfLayer& L = tf_[i];
-      run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w.partial, s);
+      run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s);
       if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
       attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
-      run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w.partial, s);
+      run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s);
       layernorm(a, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_, s);
-      run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w.partial, s);
-      run_gemm(L.ff2, ff, T, ffn_, a, D_, true, Act::None, hf, true, D_, w.partial, s);
+      run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w, s);
+      run_gemm(L.ff2, ff, T, ffn_, a, D_, true, Act::None, hf, true, D_, w, s);
       if (i + 1 < layers_)
         layernorm(a, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_,
                   s);
@@ -772,21 +806,21 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     void* const* buf = w.bufs.data();
     float* x = static_cast<float*>(buf[2]);
     run_gemm(patch_proj_, buf[0], B * npatch_, patch_proj_.k, buf[1], D_, true, Act::None, nullptr, false, 0,
-             w.partial, s);
+             w, s);
     vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     for (const TfLayer& L : tf_) {
       layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
                 f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
-      run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w.partial, s);
+      run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s);
       if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
       attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
-      run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w.partial, s);
+      run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s);
       layernorm(x, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
                 f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
-      run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w.partial, s);
-      run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w.partial, s);
+      run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s);
+      run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w, s);
     }
     // final LN on the class-token rows only (torchvision: x = ln(x); x = x[:, 0])
     layernorm(x, S * D_, ptr<float>(final_ln_.g), ptr<float>(final_ln_.b),
@@ -796,14 +830,14 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
 
 void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
-    run_gemm(fc_, w.bufs[6], B, feat_, out[0], classes_, true, Act::None, nullptr, false, 0, w.partial, s);
+    run_gemm(fc_, w.bufs[6], B, feat_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const TfLayer& L = tf_.back();
     const int T = B * S;
     layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
               static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
   } else if (family_ == SPI_FAMILY_VIT) {
-    run_gemm(head_, w.bufs[7], B, D_, out[0], classes_, true, Act::None, nullptr, false, 0, w.partial, s);
+    run_gemm(head_, w.bufs[7], B, D_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);
   }
 }
 

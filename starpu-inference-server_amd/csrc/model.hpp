@@ -23,11 +23,13 @@ struct ConvW {
   size_t w = 0, b = 0;  // blob offsets (packed weight, fp32 bias)
   int cout = 0, cin = 0, cin_pad = 0, kh = 1, kw = 1, stride = 1, pad = 0;
   int kpad = 0, npad = 0;
+  size_t wplane = 0;
 };
 
 struct LinearW {
   size_t w = 0, b = 0;
   int n = 0, k = 0, kpad = 0, npad = 0;
+  size_t wplane = 0;
   bool has_bias = true;
 };
 
@@ -94,10 +96,10 @@ class Model {
   void prologue(Workspace& w, int batch, int S, const void* const* in, hipStream_t s);
   void epilogue(Workspace& w, int batch, int S, void* const* out, hipStream_t s);
   void run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc,
-                bool out_f32, Act act, const void* res, bool res_f32, int ldr, float* partial,
+                bool out_f32, Act act, const void* res, bool res_f32, int ldr, Workspace& ws,
                 hipStream_t s);
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
-                Act act, const void* res, float* partial, hipStream_t s);
+                Act act, const void* res, Workspace& ws, hipStream_t s);
   size_t conv_partial(const ConvW& c, int B, int H, int W) const;
   size_t linear_partial(const LinearW& L, int M) const;
   template <typename P>
@@ -107,7 +109,8 @@ class Model {
 
   int device_ = 0;
   int family_ = 0;
-  bool f16_ = true;
+  Prec prec_ = Prec::F16;
+  bool f16_ = true;  // activations stored as fp16 (Prec::F16 only)
   int max_batch_ = 1;
   bool graphs_ = false;
   std::string desc_;

@@ -10,6 +10,10 @@ namespace spi {
 
 enum class Act : int { None = 0, Relu = 1, Gelu = 2 };
 
+// Contraction precision.  F16X3 = split fp16 (fp32 activations, hi/lo fp16
+// operands, three MFMAs per fragment): fp32-grade results at the fp16 rate.
+enum class Prec : int { F32 = 0, F16 = 1, F16X3 = 2 };
+
 // C[M,N] = act(A[M,K] . W[N,K]^T + bias[N] + residual[M,N])
 //
 // A is either a dense row-major activation (lda) or, for conv-as-implicit-GEMM,
@@ -19,6 +23,7 @@ enum class Act : int { None = 0, Relu = 1, Gelu = 2 };
 struct GemmDesc {
   int M = 0, N = 0, K = 0;  // logical sizes
   int Kpad = 0;             // W row stride (multiple of 64)
+  size_t wplane = 0;        // elements between the hi and lo weight planes (F16X3)
   int lda = 0;              // dense A row stride (elements)
   int ldc = 0;              // C row stride (elements)
   int ldr = 0;              // residual row stride (elements)
@@ -36,12 +41,14 @@ struct GemmPtrs {
   const float* bias = nullptr;
   const void* res = nullptr;
   void* C = nullptr;
-  float* partial = nullptr;  // split-K workspace: splits * M * N floats
+  float* partial = nullptr;  // split-K slabs (gemm_partial_floats)
+  int* counters = nullptr;   // split-K arrival tickets, zero-initialised (gemm_counter_slots)
 };
 
-// Workspace floats needed by a GEMM with the chosen split-K.
-size_t gemm_partial_floats(const GemmDesc& d, bool f16);
-void gemm(const GemmDesc& d, const GemmPtrs& p, bool f16, hipStream_t s);
+// Workspace needed by a GEMM with the chosen split-K (0 when not split).
+size_t gemm_partial_floats(const GemmDesc& d);
+size_t gemm_counter_slots(const GemmDesc& d);
+void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s);
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
