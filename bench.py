@@ -41,7 +41,7 @@ WORKLOADS = {
     "resnet152": "ResNet-152 bs=32 fp16, StarPU-style HIP workers per MI355X (request-parallel, no RCCL)",
     "vit_l_16": "ViT-L/16 224^2 bs=16 fp16 (patch-embed GEMM + MFMA attention, LDS-tiled)",
 }
-PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"fp16": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet18", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp16x3", "fp32"])
     ap.add_argument("--workers", type=int, default=4, help="worker streams per GPU")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")

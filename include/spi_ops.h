@@ -1,0 +1,58 @@
+/*
+ * spi_ops.h — op-level C entry points of the MI355X kernels.
+ *
+ * Not part of the codelet boundary (that is spi_codelet.h): these expose the
+ * individual HIP kernels the forward passes are built from, for kernel-level
+ * parity tests against a plain fp32 reference and for micro-benchmarks.  All
+ * pointers are device pointers unless marked host; every call only enqueues
+ * on `stream`.  Return 0 on success, non-zero on invalid arguments / HIP error
+ * (message in spi_last_error()).
+ */
+#ifndef SPI_OPS_H
+#define SPI_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Packed weight layout for a [N][K] fp32 matrix: rows padded to Npad = 128k,
+ * columns to Kpad = 64k; fp16 / fp32 elements, or for fp16x3 per 32-k block
+ * [32 hi fp16 | 32 lo fp16].  Returns the packed byte count; writes Npad/Kpad. */
+size_t spi_op_packed_bytes(int32_t precision, int32_t N, int32_t K, int32_t* Npad, int32_t* Kpad);
+/* Host-side packing: w_host fp32 [N][K] -> dst_host (spi_op_packed_bytes bytes). */
+int spi_op_pack_weight(int32_t precision, const float* w_host, int32_t N, int32_t K, void* dst_host);
+
+/* Bytes of device scratch a GEMM / conv call needs (zero line, split-K slabs
+ * and tickets).  The scratch must be zero-filled once before first use. */
+size_t spi_op_workspace_bytes(void);
+
+/* C[M,N] = act(A[M,K] . W^T + bias + residual); act: 0 none, 1 relu, 2 gelu.
+ * A: fp16 (precision fp16) or fp32 (fp32 / fp16x3), row stride lda.
+ * residual: same element type as A unless res_f32; C: fp32 when out_f32. */
+int spi_op_gemm(int32_t precision, const void* A, int32_t M, int32_t K, int32_t lda,
+                const void* W_packed, int32_t N, const float* bias, const void* residual,
+                int32_t res_f32, int32_t ldr, void* C, int32_t out_f32, int32_t ldc,
+                int32_t act, void* workspace, void* stream);
+
+/* NHWC conv as implicit GEMM: x [B][H][W][Cin] (Cin a power of two >= 8,
+ * >= 4 for fp32), W packed from [Cout][KH][KW][Cin] order, y [B][OH][OW][Cout]. */
+int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_t W,
+                  int32_t Cin, const void* W_packed, int32_t Cout, int32_t KH, int32_t KW,
+                  int32_t stride, int32_t pad, const float* bias, const void* residual,
+                  void* y, int32_t act, void* workspace, void* stream);
+
+/* Multi-head attention over packed qkv [B*S][3*D] (fp16 or fp32), head_dim 64. */
+int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias, void* ctx,
+                     int32_t B, int32_t S, int32_t heads, float scale, void* stream);
+
+/* Row LayerNorm: x fp32 [rows][D] -> yf fp32 and/or yt (fp16 when precision fp16). */
+int spi_op_layernorm(int32_t precision, const float* x, const float* gamma, const float* beta,
+                     float* yf, void* yt, int32_t rows, int32_t D, float eps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPI_OPS_H */

@@ -189,6 +189,21 @@ _PROTOS = {
     "spi_stream_destroy": (None, [C.c_void_p]),
     "spi_stream_synchronize": (C.c_int, [C.c_void_p]),
     "spi_last_error": (C.c_char_p, []),
+    # include/spi_ops.h
+    "spi_op_packed_bytes": (C.c_size_t, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32)]),
+    "spi_op_pack_weight": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
+    "spi_op_workspace_bytes": (C.c_size_t, []),
+    "spi_op_gemm": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                              C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                              C.c_int32, C.c_void_p, C.c_void_p]),
+    "spi_op_conv2d": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "spi_op_attention": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_float, C.c_void_p]),
+    "spi_op_layernorm": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_int32, C.c_int32, C.c_float, C.c_void_p]),
 }
 
 

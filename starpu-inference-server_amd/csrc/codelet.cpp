@@ -206,6 +206,7 @@ void spi_set_worker_context(int32_t worker_id, int32_t device_id, void* hip_stre
 void spi_clear_worker_context(void) { tl_ctx = WorkerContext{}; }
 
 const char* spi_last_error(void) { return tl_last_error.c_str(); }
+void spi_set_last_error(const char* msg) { tl_last_error = msg ? msg : ""; }
 
 void spi_hip_inference_func(void** buffers, void* cl_arg) {
   auto* a = static_cast<spi_codelet_args*>(cl_arg);

@@ -3,69 +3,75 @@
 // One kernel body serves every dense contraction of the three model families:
 //   * ResNet conv + folded BN (+ residual) (+ ReLU)      -- implicit GEMM over NHWC
 //   * ResNet FC, BERT/ViT QKV / out-proj / FFN (+GELU) (+residual) -- dense GEMM
-// Operands are K-contiguous on both sides (activations [M][K], weights packed
-// [Npad][Kpad]), so each lane's MFMA fragment is one 16-byte chunk.
 //
-// Precision modes (template MODE):
-//   F16   v_mfma_f32_16x16x32_f16; lane l holds A[row l&15][k 8(l>>4)..+7].
-//   F32   v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain); lane l feeds k index
-//         (l>>4) of step s with element 8(l>>4)+s of its 32-byte chunk (the k
-//         order is permuted identically on A and B, so the sum is unchanged).
-//   F16X3 split fp16: fp32 activations are split on the way into LDS as
-//         a = a_hi + a_lo (two fp16), weights are stored as two fp16 planes,
-//         and each fragment issues hi*hi + hi*lo + lo*hi (the lo*lo term is
-//         below fp32 rounding): fp32-grade results at the fp16 MFMA rate.
-// Accumulators follow the gfx950 C/D map: col = lane&15, row = 4(lane>>4)+r.
+// Staging.  Every k-step moves 128 bytes of each A row and each W row:
+//   F16   64 fp16 k-values (2 x v_mfma_f32_16x16x32_f16 per fragment pair)
+//   F32   32 fp32 k-values (8 x v_mfma_f32_16x16x4_f32; lane l feeds k index
+//         (l>>4) of step s with element 8(l>>4)+s of its 32 bytes -- the same
+//         permutation on A and B, so the sum is unchanged; exact fp32 FMA chain)
+//   F16X3 32 fp32 A values + W row = 32 hi fp16 | 32 lo fp16 (interleaved
+//         packing); A is split into hi/lo at fragment-read time; each fragment
+//         pair issues lo*hi + hi*lo + hi*hi (fp32-grade at the fp16 rate).
+// The tile images are filled with global_load_lds_dwordx4 (LDS-DMA, 1 KiB per
+// wave instruction, lane-linear): image row r, 16-byte slot s holds global chunk
+// s ^ (r & 7) -- the XOR swizzle is applied on the SOURCE address and undone on
+// the ds_read_b128 (cdna_hip_programming.md rule 21), which makes the fp16
+// fragment reads bank-conflict free.  Chunks outside the image (conv padding,
+// rows past M, k past K) are read from a zeroed line, so the DMA never needs a
+// predicate.  STAGES-deep ring: step t+STAGES-1 is issued right after the
+// barrier that publishes step t, waits are counted vmcnt + s_barrier in one
+// asm statement (no __syncthreads(): its vmcnt(0) would drain the prefetch).
 //
-// Tiles are staged global -> registers -> LDS (double-buffered, one barrier per
-// 32-deep K step, next tile's loads issued before the current tile's MFMAs).
-// Small-M layers are split along K; the workgroups of a tile publish fp32
-// slabs and the last one to arrive (agent-scope release -> ticket -> acquire,
-// cdna_hip_programming.md G16 / "In-launch split-K reduction") sums them and
-// runs the epilogue, so no separate reduce launch is needed.
+// Small-M layers are split along K; the workgroups of a tile publish fp32 slabs
+// write-through (sc1) and the last to arrive (relaxed agent-scope ticket) sums
+// them with sc1 loads and runs the epilogue -- no second launch, no cache-wide
+// fences (cdna_hip_programming.md, "In-launch split-K reduction").
 #include "spi_kernels.hpp"
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 namespace spi {
 namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int BK = 32;
+constexpr int ROWB = 128;  // bytes per image row per k-step
 
 struct KArgs {
   GemmDesc d;
   GemmPtrs p;
-  int k_per_split;
+  int k_per_split;  // elements, multiple of the k-step
   int tiles_m;
+  int tiles;
   int cin_shift;
+  int kw_mul;       // ceil(65536 / KW): cell / KW == (cell * kw_mul) >> 16 for cell < 2^12
+  int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
 };
 
 template <int MODE>
 struct Traits;
 template <>
 struct Traits<(int)Prec::F16> {
-  using A = _Float16;   // A element in HBM
-  using L = _Float16;   // LDS / MFMA operand element
-  using Out = _Float16; // default C / residual element
-  static constexpr int KC = 8, PLANES = 1, AV = 1;  // k per chunk, weight planes, uint4 per A chunk
+  using A = _Float16;
+  using Out = _Float16;
+  static constexpr int ESTEP = 64, EPC = 8;  // k per step, A elements per 16-B chunk
 };
 template <>
 struct Traits<(int)Prec::F32> {
   using A = float;
-  using L = float;
   using Out = float;
-  static constexpr int KC = 4, PLANES = 1, AV = 1;
+  static constexpr int ESTEP = 32, EPC = 4;
 };
 template <>
 struct Traits<(int)Prec::F16X3> {
   using A = float;
-  using L = _Float16;
   using Out = float;
-  static constexpr int KC = 8, PLANES = 2, AV = 2;
+  static constexpr int ESTEP = 32, EPC = 4;
 };
 
 __device__ __forceinline__ float apply_act(float v, Act act) {
@@ -91,187 +97,205 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, int m, int n, flo
     static_cast<Out*>(a.p.C)[(size_t)m * d.ldc + n] = static_cast<Out>(v);
 }
 
-__device__ __forceinline__ void split8(const uint4& x0, const uint4& x1, uint4& hi, uint4& lo) {
-  const float* f0 = reinterpret_cast<const float*>(&x0);
-  const float* f1 = reinterpret_cast<const float*>(&x1);
-  half8 h, l;
+__device__ __forceinline__ void split8(const u32x4& x0, const u32x4& x1, half8& hi, half8& lo) {
+  const floatx4 f0 = __builtin_bit_cast(floatx4, x0);
+  const floatx4 f1 = __builtin_bit_cast(floatx4, x1);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const _Float16 a = static_cast<_Float16>(f0[e]);
     const _Float16 b = static_cast<_Float16>(f1[e]);
-    h[e] = a;
-    h[e + 4] = b;
-    l[e] = static_cast<_Float16>(f0[e] - static_cast<float>(a));
-    l[e + 4] = static_cast<_Float16>(f1[e] - static_cast<float>(b));
+    hi[e] = a;
+    hi[e + 4] = b;
+    lo[e] = static_cast<_Float16>(f0[e] - static_cast<float>(a));
+    lo[e + 4] = static_cast<_Float16>(f1[e] - static_cast<float>(b));
   }
-  hi = *reinterpret_cast<uint4*>(&h);
-  lo = *reinterpret_cast<uint4*>(&l);
 }
 
-template <int MODE, int BM, int BN, bool CONV>
+// Wait for this wave's LDS-DMA down to N outstanding, then barrier.  One asm
+// statement with a memory clobber so no LDS access moves across it.
+template <int N>
+__device__ __forceinline__ void dma_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
+  return *reinterpret_cast<const u32x4*>(img + row * ROWB + ((c ^ (row & 7)) << 4));
+}
+
+template <int MODE, int BM, int BN, int STAGES, bool CONV>
 __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   using TR = Traits<MODE>;
   using AT = typename TR::A;
-  using LT = typename TR::L;
-  constexpr int KC = TR::KC;
-  constexpr int CPR = BK / KC;                 // chunks per tile row
-  constexpr int LPAD = 16 / (int)sizeof(LT);   // 16-byte row pad
-  constexpr int LD = BK + LPAD;                // LDS row stride (elements)
-  constexpr int A_PER_T = BM * CPR / 256;
-  constexpr int B_PER_T = BN * CPR / 256;
-  static_assert(A_PER_T >= 1 && B_PER_T >= 1, "tile too small");
-  constexpr int PL = TR::PLANES;
-  constexpr int PLANE = (BM + BN) * LD;        // one precision plane of one buffer
-  constexpr int BUF = PL * PLANE;
-  __shared__ __attribute__((aligned(16))) LT lds[2 * BUF];
-  __shared__ int s_last;
+  constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC;
+  constexpr int IMG = (BM + BN) * ROWB;  // bytes per stage
+  constexpr int AQ = BM / 32, BQ = BN / 32;  // DMA instructions per wave per step
+  constexpr int QPS = AQ + BQ;
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * IMG + 16];
+  int* s_flag = reinterpret_cast<int*>(lds + STAGES * IMG);
 
   const GemmDesc& d = a.d;
-  const int tid = threadIdx.x;
-  const int tile = blockIdx.x;
-  const int tm = tile % a.tiles_m;
-  const int tn = tile / a.tiles_m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
+  int tile = blockIdx.x;
+  {
+    const int nwg = a.tiles, q = nwg >> 3, r = nwg & 7, x = tile & 7, l = tile >> 3;
+    if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+  }
+  const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.y * a.k_per_split;
   const int kend = min(d.Kpad, kbeg + a.k_per_split);
-  const int ntiles = (kend - kbeg) / BK;
+  const int nsteps = (kend - kbeg) / ESTEP;
 
+  const char* zeros = static_cast<const char*>(a.p.zeros);
   const AT* __restrict__ Ap = static_cast<const AT*>(a.p.A);
-  const LT* __restrict__ Wp = static_cast<const LT*>(a.p.W);
+  const char* __restrict__ Wb = static_cast<const char*>(a.p.W);
 
-  int a_row[A_PER_T], a_kc[A_PER_T], a_ih0[A_PER_T], a_iw0[A_PER_T];
-  bool a_ok[A_PER_T];
-  size_t a_base[A_PER_T];
+  // Per-lane source bookkeeping (fixed across k-steps).
+  const int slot = lane & 7;
+  int a_koff[AQ], a_ih0[AQ], a_iw0[AQ];
+  bool a_ok[AQ];
+  const AT* a_base[AQ];
+  const AT* a_pix[AQ];  // conv: image pointer at (ih0, iw0), may point before the image
 #pragma unroll
-  for (int t = 0; t < A_PER_T; ++t) {
-    const int c = tid + t * 256;
-    a_row[t] = c / CPR;
-    a_kc[t] = c % CPR;
-    const int m = m0 + a_row[t];
-    a_ok[t] = m < d.M;
+  for (int q = 0; q < AQ; ++q) {
+    const int r = (wave * AQ + q) * 8 + (lane >> 3);
+    a_koff[q] = (slot ^ (r & 7)) * EPC;
+    const int m = m0 + r;
+    a_ok[q] = m < d.M;
+    const int mm = a_ok[q] ? m : 0;
     if constexpr (CONV) {
       const int ohw = d.OH * d.OW;
-      const int mm = a_ok[t] ? m : 0;
       const int img = mm / ohw;
       const int rem = mm - img * ohw;
       const int oh = rem / d.OW;
       const int ow = rem - oh * d.OW;
-      a_ih0[t] = oh * d.stride - d.pad;
-      a_iw0[t] = ow * d.stride - d.pad;
-      a_base[t] = (size_t)img * d.H * d.W * d.Cin;
+      a_ih0[q] = oh * d.stride - d.pad;
+      a_iw0[q] = ow * d.stride - d.pad;
+      a_base[q] = Ap + (size_t)img * d.H * d.W * d.Cin;
+      a_pix[q] = a_base[q] + ((ptrdiff_t)(a_ih0[q] * d.W + a_iw0[q]) << a.cin_shift);
     } else {
-      a_ih0[t] = a_iw0[t] = 0;
-      a_base[t] = (size_t)(a_ok[t] ? m : 0) * d.lda;
+      a_ih0[q] = a_iw0[q] = 0;
+      a_base[q] = Ap + (size_t)mm * d.lda;
+      a_pix[q] = a_base[q];
     }
   }
+  const char* b_src[BQ];
+#pragma unroll
+  for (int q = 0; q < BQ; ++q) {
+    const int r = (wave * BQ + q) * 8 + (lane >> 3);
+    const int c = slot ^ (r & 7);
+    // W rows are Kpad elements (F16/F32) or 2*Kpad fp16 (F16X3, 64-element blocks of hi|lo).
+    const size_t row_bytes = (MODE == (int)Prec::F16) ? (size_t)d.Kpad * 2 : (size_t)d.Kpad * 4;
+    b_src[q] = Wb + (size_t)(n0 + r) * row_bytes + c * 16;
+  }
 
-  uint4 ra[A_PER_T][TR::AV], rb[B_PER_T][PL];
-  auto load_tile = [&](int k0) {
+  auto issue = [&](int step, int stage) {
+    const int k0 = kbeg + step * ESTEP;
+    char* dst = lds + stage * IMG;
+    if constexpr (CONV) {
+      if (a.cell_uniform) {
+        // Cin >= k-step: the whole step sits in one (kh, kw) cell -> scalar math.
+        const int cell = k0 >> a.cin_shift;
+        const int kh = (cell * a.kw_mul) >> 16;
+        const int kw = cell - kh * d.KW;
+        const ptrdiff_t step_off = ((ptrdiff_t)(kh * d.W + kw) << a.cin_shift) + (k0 & (d.Cin - 1));
+        const bool k_ok = k0 < d.K;
 #pragma unroll
-    for (int t = 0; t < A_PER_T; ++t) {
-      const int k = k0 + a_kc[t] * KC;
-#pragma unroll
-      for (int v = 0; v < TR::AV; ++v) ra[t][v] = make_uint4(0, 0, 0, 0);
-      if (a_ok[t] && k < d.K) {
-        const AT* src = nullptr;
-        if constexpr (CONV) {
-          const int cell = k >> a.cin_shift;
-          const int c = k & (d.Cin - 1);
-          const int kh = cell / d.KW;
-          const int kw = cell - kh * d.KW;
-          const int ih = a_ih0[t] + kh, iw = a_iw0[t] + kw;
-          if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W)
-            src = Ap + a_base[t] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c;
-        } else {
-          src = Ap + a_base[t] + k;
+        for (int q = 0; q < AQ; ++q) {
+          const int ih = a_ih0[q] + kh, iw = a_iw0[q] + kw;
+          const bool ok = k_ok && a_ok[q] && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
+          const char* src = ok ? reinterpret_cast<const char*>(a_pix[q] + step_off + a_koff[q]) : zeros;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
-        if (src) {
-#pragma unroll
-          for (int v = 0; v < TR::AV; ++v) ra[t][v] = reinterpret_cast<const uint4*>(src)[v];
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < B_PER_T; ++t) {
-      const int c = tid + t * 256;
-      const int row = c / CPR, kc = c % CPR;
-      const LT* src = Wp + (size_t)(n0 + row) * d.Kpad + k0 + kc * KC;
-#pragma unroll
-      for (int p = 0; p < PL; ++p) rb[t][p] = *reinterpret_cast<const uint4*>(src + (size_t)p * d.wplane);
-    }
-  };
-  auto store_tile = [&](int buf) {
-    LT* base = lds + buf * BUF;
-#pragma unroll
-    for (int t = 0; t < A_PER_T; ++t) {
-      LT* dst = base + a_row[t] * LD + a_kc[t] * KC;
-      if constexpr (MODE == (int)Prec::F16X3) {
-        uint4 hi, lo;
-        split8(ra[t][0], ra[t][1], hi, lo);
-        *reinterpret_cast<uint4*>(dst) = hi;
-        *reinterpret_cast<uint4*>(dst + PLANE) = lo;
       } else {
-        *reinterpret_cast<uint4*>(dst) = ra[t][0];
+#pragma unroll
+        for (int q = 0; q < AQ; ++q) {
+          const char* src = zeros;
+          const int k = k0 + a_koff[q];
+          if (a_ok[q] && k < d.K) {
+            const int cell = k >> a.cin_shift;
+            const int c = k & (d.Cin - 1);
+            const int kh = (cell * a.kw_mul) >> 16;
+            const int kw = cell - kh * d.KW;
+            const int ih = a_ih0[q] + kh, iw = a_iw0[q] + kw;
+            if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W)
+              src = reinterpret_cast<const char*>(a_base[q] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c);
+          }
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < AQ; ++q) {
+        const int k = k0 + a_koff[q];
+        const char* src = (a_ok[q] && k < d.K) ? reinterpret_cast<const char*>(a_pix[q] + k) : zeros;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
+    // k-step byte offset inside a W row: 128 B per step in every mode.
+    const size_t kb = (size_t)(k0 / ESTEP) * ROWB;
 #pragma unroll
-    for (int t = 0; t < B_PER_T; ++t) {
-      const int c = tid + t * 256;
-      const int row = c / CPR, kc = c % CPR;
-      LT* dst = base + (BM + row) * LD + kc * KC;
-#pragma unroll
-      for (int p = 0; p < PL; ++p) *reinterpret_cast<uint4*>(dst + p * PLANE) = rb[t][p];
-    }
+    for (int q = 0; q < BQ; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[q] + kb),
+                                       (lds_ptr_t)(dst + BM * ROWB + (wave * BQ + q) * 1024), 16, 0, 0);
   };
 
-  const int lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TI = WTM / 16, TJ = WTN / 16;
-  const int fr = lane & 15, fq = lane >> 4;
   floatx4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  if (ntiles > 0) {
-    load_tile(kbeg);
-    store_tile(0);
-  }
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nsteps) issue(s, s);
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) load_tile(kbeg + (t + 1) * BK);
-    const LT* As = lds + cur * BUF;
-    const LT* Bs = As + BM * LD;
+  for (int t = 0; t < nsteps; ++t) {
+    // Step t has landed once at most (issued steps after t) DMA groups remain.
+    if constexpr (STAGES == 3) {
+      if (t + 1 < nsteps)
+        dma_wait_barrier<QPS>();
+      else
+        dma_wait_barrier<0>();
+    } else {
+      dma_wait_barrier<0>();
+    }
+    if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    const char* As = lds + (t % STAGES) * IMG;
+    const char* Bs = As + BM * ROWB;
     if constexpr (MODE == (int)Prec::F16) {
-      half8 af[TI], bf[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
-        af[i] = *reinterpret_cast<const half8*>(As + (wm * WTM + i * 16 + fr) * LD + fq * 8);
+      for (int kk = 0; kk < 2; ++kk) {
+        half8 af[TI], bf[TJ];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        bf[j] = *reinterpret_cast<const half8*>(Bs + (wn * WTN + j * 16 + fr) * LD + fq * 8);
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
+          af[i] = __builtin_bit_cast(half8, rd_chunk(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          bf[j] = __builtin_bit_cast(half8, rd_chunk(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
     } else if constexpr (MODE == (int)Prec::F16X3) {
       half8 ah[TI], al[TI], bh[TJ], bl[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const LT* s = As + (wm * WTM + i * 16 + fr) * LD + fq * 8;
-        ah[i] = *reinterpret_cast<const half8*>(s);
-        al[i] = *reinterpret_cast<const half8*>(s + PLANE);
+        const int row = wm * WTM + i * 16 + fr;
+        split8(rd_chunk(As, row, 2 * fq), rd_chunk(As, row, 2 * fq + 1), ah[i], al[i]);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const LT* s = Bs + (wn * WTN + j * 16 + fr) * LD + fq * 8;
-        bh[j] = *reinterpret_cast<const half8*>(s);
-        bl[j] = *reinterpret_cast<const half8*>(s + PLANE);
+        const int row = wn * WTN + j * 16 + fr;
+        bh[j] = __builtin_bit_cast(half8, rd_chunk(Bs, row, fq));
+        bl[j] = __builtin_bit_cast(half8, rd_chunk(Bs, row, 4 + fq));
       }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
@@ -285,15 +309,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
       floatx4 a0[TI], a1[TI], b0[TJ], b1[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const float* src = reinterpret_cast<const float*>(As) + (wm * WTM + i * 16 + fr) * LD + fq * 8;
-        a0[i] = *reinterpret_cast<const floatx4*>(src);
-        a1[i] = *reinterpret_cast<const floatx4*>(src + 4);
+        const int row = wm * WTM + i * 16 + fr;
+        a0[i] = __builtin_bit_cast(floatx4, rd_chunk(As, row, 2 * fq));
+        a1[i] = __builtin_bit_cast(floatx4, rd_chunk(As, row, 2 * fq + 1));
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const float* src = reinterpret_cast<const float*>(Bs) + (wn * WTN + j * 16 + fr) * LD + fq * 8;
-        b0[j] = *reinterpret_cast<const floatx4*>(src);
-        b1[j] = *reinterpret_cast<const floatx4*>(src + 4);
+        const int row = wn * WTN + j * 16 + fr;
+        b0[j] = __builtin_bit_cast(floatx4, rd_chunk(Bs, row, 2 * fq));
+        b1[j] = __builtin_bit_cast(floatx4, rd_chunk(Bs, row, 2 * fq + 1));
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -310,8 +334,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][s], b1[j][s], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < ntiles) store_tile(cur ^ 1);
-    __syncthreads();
   }
 
   if (gridDim.y == 1) {
@@ -332,9 +354,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   // Slabs are written in fragment order (thread tid's accumulator (i, j) is 16
   // contiguous bytes at ((i*TJ + j)*256 + tid)*16), write-through (sc1) so no
   // release fence is needed; the ticket is a relaxed agent-scope atomic; the
-  // reducer reads every slab with sc1 loads (cdna_hip_programming.md, "In-launch
-  // split-K reduction", sc1 variant).  Same thread <-> (m, n) map as above.
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  // reducer reads every slab with sc1 loads.  Same thread <-> (m, n) map as above.
   const int splits = gridDim.y;
   constexpr int SLAB = BM * BN;
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
@@ -347,57 +367,80 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
       const int off = (blockIdx.y * SLAB + ((i * TJ + j) * 256 + tid) * 4) * 4;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
     }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (tid == 0) {
     const int ticket = __hip_atomic_fetch_add(a.p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = ticket == splits - 1;
-    if (s_last) __hip_atomic_store(a.p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == splits - 1;
+    if (last) __hip_atomic_store(a.p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!*s_flag) return;
+  // Four splits' slabs in flight per round; loads past the last slab fall
+  // outside the descriptor's range and return 0 (no branch, no per-load wait).
+  floatx4 sum[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
-      for (int z = 0; z < splits; ++z) {
-        const int off = (z * SLAB + ((i * TJ + j) * 256 + tid) * 4) * 4;
-        sum += __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-      }
+    for (int j = 0; j < TJ; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int z0 = 0; z0 < splits; z0 += 4) {
+    floatx4 v[4][TI][TJ];
+#pragma unroll
+    for (int zz = 0; zz < 4; ++zz)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * 256 + tid) * 4) * 4;
+          v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+        }
+#pragma unroll
+    for (int zz = 0; zz < 4; ++zz)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) sum[i][j] += v[zz][i][j];
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
         const int n = n0 + wn * WTN + j * 16 + fr;
-        if (m < d.M && n < d.N) epilogue_store<MODE>(a, m, n, sum[r]);
+        if (m < d.M && n < d.N) epilogue_store<MODE>(a, m, n, sum[i][j][r]);
       }
-    }
 }
 
 struct Plan {
-  int bm, bn, splits, k_per_split;
+  int bm, bn, stages, splits, k_per_split;
 };
 
-Plan choose_plan(const GemmDesc& d) {
+int estep_of(Prec prec) { return prec == Prec::F16 ? 64 : 32; }
+
+Plan choose_plan(const GemmDesc& d, Prec prec) {
   constexpr int kTarget = 256;  // CUs
+  const int ES = estep_of(prec);
   static const int cfg[3][2] = {{128, 128}, {128, 64}, {64, 64}};
-  Plan pl{64, 64, 1, d.Kpad};
+  Plan pl{64, 64, 3, 1, d.Kpad};
   for (auto& c : cfg) {
     if (c[1] == 128 && d.N <= 64) continue;
     const int tiles = ((d.M + c[0] - 1) / c[0]) * ((d.N + c[1] - 1) / c[1]);
     if (tiles >= kTarget) {
       pl.bm = c[0];
       pl.bn = c[1];
+      pl.stages = (c[0] == 128 && c[1] == 128) ? 2 : 3;
       return pl;
     }
   }
   const int tiles = ((d.M + 63) / 64) * ((d.N + 63) / 64);
-  const int ktiles = d.Kpad / BK;
+  const int ksteps = d.Kpad / ES;
   int splits = 1;
-  if (tiles < kTarget / 2 && ktiles >= 8) splits = std::max(1, std::min(ktiles / 4, (2 * kTarget + tiles - 1) / tiles));
-  const int kt_per = (ktiles + splits - 1) / splits;
-  pl.k_per_split = kt_per * BK;
-  pl.splits = (ktiles + kt_per - 1) / kt_per;
+  if (tiles < kTarget / 2 && ksteps >= 6) splits = std::max(1, std::min(ksteps / 3, (2 * kTarget + tiles - 1) / tiles));
+  const int kt_per = (ksteps + splits - 1) / splits;
+  pl.k_per_split = kt_per * ES;
+  pl.splits = (ksteps + kt_per - 1) / kt_per;
   return pl;
 }
 
@@ -407,42 +450,51 @@ int ilog2(int v) {
   return s;
 }
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int STAGES>
 void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
   if (a.d.conv)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, true>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, true>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, false>), grid, dim3(256), 0, s, a);
 }
 
 template <int MODE>
 void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
-  const Plan pl = choose_plan(d);
-  KArgs a{d, p, pl.k_per_split, (d.M + pl.bm - 1) / pl.bm, d.conv ? ilog2(d.Cin) : 0};
-  const int tiles_n = (d.N + pl.bn - 1) / pl.bn;
-  const dim3 grid(a.tiles_m * tiles_n, pl.splits);
+  const Plan pl = choose_plan(d, (Prec)MODE);
+  KArgs a{};
+  a.d = d;
+  a.p = p;
+  a.k_per_split = pl.k_per_split;
+  a.tiles_m = (d.M + pl.bm - 1) / pl.bm;
+  a.tiles = a.tiles_m * ((d.N + pl.bn - 1) / pl.bn);
+  a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
+  a.kw_mul = (65536 + d.KW - 1) / d.KW;
+  a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP;
+  const dim3 grid(a.tiles, pl.splits);
   if (pl.bm == 128 && pl.bn == 128)
-    launch_tile<MODE, 128, 128>(a, grid, s);
+    launch_tile<MODE, 128, 128, 2>(a, grid, s);
   else if (pl.bm == 128)
-    launch_tile<MODE, 128, 64>(a, grid, s);
+    launch_tile<MODE, 128, 64, 3>(a, grid, s);
   else
-    launch_tile<MODE, 64, 64>(a, grid, s);
+    launch_tile<MODE, 64, 64, 3>(a, grid, s);
 }
 
 }  // namespace
 
-size_t gemm_partial_floats(const GemmDesc& d) {
-  const Plan pl = choose_plan(d);
+size_t gemm_partial_floats(const GemmDesc& d, Prec prec) {
+  const Plan pl = choose_plan(d, prec);
   if (pl.splits <= 1) return 0;
   const size_t tiles = (size_t)((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
   return tiles * pl.splits * pl.bm * pl.bn;
 }
 
-size_t gemm_counter_slots(const GemmDesc& d) {
-  const Plan pl = choose_plan(d);
+size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
+  const Plan pl = choose_plan(d, prec);
   if (pl.splits <= 1) return 0;
   return (size_t)((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
 }
+
+int gemm_kstep(Prec prec) { return estep_of(prec); }
 
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   switch (prec) {

@@ -6,6 +6,7 @@
 // reference exports (models/import_resnet.py:25-73, models/import_vit.py:10-62,
 // models/import_bert-base-uncased.py:8-39).
 #include "model.hpp"
+#include "pack.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -97,24 +98,8 @@ Blob* g_blob = nullptr;  // only used during construction (single thread)
 // compute type.  get(n, k) supplies element (n, k) in packed-k order.
 template <typename F>
 size_t pack_matrix(int N, int K, int Npad, int Kpad, Prec prec, F get) {
-  const size_t plane = (size_t)Npad * Kpad;
-  const size_t bytes = prec == Prec::F32 ? plane * 4 : prec == Prec::F16 ? plane * 2 : plane * 4;
-  const size_t off = g_blob->add(nullptr, bytes);
-  char* dst = g_blob->at(off);
-  std::memset(dst, 0, bytes);
-  for (int n = 0; n < N; ++n)
-    for (int k = 0; k < K; ++k) {
-      const float v = get(n, k);
-      const size_t i = (size_t)n * Kpad + k;
-      if (prec == Prec::F32) {
-        reinterpret_cast<float*>(dst)[i] = v;
-      } else {
-        const _Float16 hi = static_cast<_Float16>(v);
-        reinterpret_cast<_Float16*>(dst)[i] = hi;
-        if (prec == Prec::F16X3)  // lo plane: the residual fp16 cannot hold
-          reinterpret_cast<_Float16*>(dst)[plane + i] = static_cast<_Float16>(v - static_cast<float>(hi));
-      }
-    }
+  const size_t off = g_blob->add(nullptr, packed_bytes(prec, Npad, Kpad));
+  pack_matrix_into(g_blob->at(off), N, K, Npad, Kpad, prec, get);
   return off;
 }
 
@@ -257,6 +242,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
   }
   Blob blob;
   g_blob = &blob;
+  blob.add(nullptr, 256);  // offset 0: zero line read by the GEMM for padded chunks
   std::ostringstream os;
   if (family_ == SPI_FAMILY_AFFINE) {
     aff_scale_ = cfg.affine_scale;
@@ -562,11 +548,11 @@ GemmDesc linear_desc(const LinearW& L, int M, int lda, int ldc) {
 
 size_t Model::conv_partial(const ConvW& c, int B, int H, int W) const {
   int OH, OW;
-  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW));
+  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW), prec_);
 }
 
 size_t Model::linear_partial(const LinearW& L, int M) const {
-  return gemm_partial_floats(linear_desc(L, M, L.k, L.n));
+  return gemm_partial_floats(linear_desc(L, M, L.k, L.n), prec_);
 }
 
 void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
@@ -588,7 +574,8 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   p.C = y;
   p.partial = ws.partial;
   p.counters = ws.counters;
-  if (gemm_partial_floats(d) > ws.partial_floats || gemm_counter_slots(d) > kCounterSlots)
+  p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
+  if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
   gemm(d, p, prec_, s);
   if (prof_) op_end(s);
@@ -616,7 +603,8 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   p.C = C;
   p.partial = ws.partial;
   p.counters = ws.counters;
-  if (gemm_partial_floats(d) > ws.partial_floats || gemm_counter_slots(d) > kCounterSlots)
+  p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
+  if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
   gemm(d, p, prec_, s);
   if (prof_) op_end(s);

@@ -19,7 +19,8 @@ enum class Prec : int { F32 = 0, F16 = 1, F16X3 = 2 };
 // A is either a dense row-major activation (lda) or, for conv-as-implicit-GEMM,
 // an NHWC image gathered on the fly: row m = (img, oh, ow), column
 // k = (kh*KW + kw)*Cin + c.  W is pre-packed [Npad][Kpad] (K contiguous,
-// zero padded), so both MFMA operands are K-contiguous 16-byte chunks.
+// zero padded), so both MFMA operands are K-contiguous 16-byte chunks.  For
+// Prec::F16X3 each W row is Kpad/32 blocks of [32 hi fp16 | 32 lo fp16].
 struct GemmDesc {
   int M = 0, N = 0, K = 0;  // logical sizes
   int Kpad = 0;             // W row stride (multiple of 64)
@@ -43,11 +44,14 @@ struct GemmPtrs {
   void* C = nullptr;
   float* partial = nullptr;  // split-K slabs (gemm_partial_floats)
   int* counters = nullptr;   // split-K arrival tickets, zero-initialised (gemm_counter_slots)
+  const void* zeros = nullptr;  // >= 16 zero bytes (source of padded / out-of-range chunks)
 };
 
 // Workspace needed by a GEMM with the chosen split-K (0 when not split).
-size_t gemm_partial_floats(const GemmDesc& d);
-size_t gemm_counter_slots(const GemmDesc& d);
+size_t gemm_partial_floats(const GemmDesc& d, Prec prec);
+size_t gemm_counter_slots(const GemmDesc& d, Prec prec);
+// k-values per staged step (W rows must be padded to a multiple of it).
+int gemm_kstep(Prec prec);
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s);
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.

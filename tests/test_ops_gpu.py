@@ -1,0 +1,124 @@
+"""Kernel-level parity: each HIP kernel (include/spi_ops.h) vs a plain fp32
+PyTorch reference of the same op.
+
+Tolerances are normalised max-abs error (max|got - ref| / max|ref|):
+fp32 (exact fp32 MFMA FMA chains) 1e-5; fp16x3 (split fp16) 1e-5; fp16 (fp16
+operands rounded from the fp32 reference inputs, fp32 accumulation) 5e-3.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle.cpu_codelet import normalized_max_error
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 5e-3}
+PRECS = ["fp32", "fp16", "fp16x3"]
+
+
+@pytest.fixture(scope="module")
+def ops(spi, gpu):
+    import importlib
+    return importlib.import_module("starpu-inference-server_amd.ops")
+
+
+def test_gemm_identity_asymmetric(ops):
+    """A = I with an asymmetric B catches a transposed C write (guide 3)."""
+    for prec in PRECS:
+        n = 64
+        A = torch.eye(n, device="cuda").to(ops.act_dtype(prec))
+        B = np.arange(n * n, dtype=np.float32).reshape(n, n) % 17 - 8  # exact in fp16
+        out = ops.gemm(prec, A, ops.pack_weight(prec, B), n)
+        np.testing.assert_array_equal(out.cpu().numpy(), B.T)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("M,N,K", [(1, 1000, 512), (8, 1000, 2048), (100, 72, 96), (1024, 768, 3072),
+                                   (392, 512, 4608), (3152, 3072, 1024)])
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+def test_gemm_bias_residual_act(ops, prec, M, N, K, act):
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    dt = ops.act_dtype(prec)
+    A_in = A.to(dt)
+    ref = A_in.float() @ (W.half().float() if prec == "fp16" else W).T + b + R
+    ref = {None: ref, "relu": F.relu(ref), "gelu": F.gelu(ref)}[act]
+    out = ops.gemm(prec, A_in.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda(), residual=R.cuda(), act=act)
+    err = normalized_max_error(out.cpu().numpy(), ref.numpy())
+    assert err < TOL[prec], f"{prec} {M}x{N}x{K} {act}: {err:.3e}"
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("B,H,cin,cout,k,stride", [(2, 224, 3, 64, 7, 2), (3, 56, 64, 64, 3, 1), (2, 56, 64, 128, 3, 2),
+                                                   (2, 14, 256, 512, 1, 2), (4, 7, 512, 512, 3, 1),
+                                                   (1, 9, 16, 24, 3, 1)])
+def test_conv2d_nhwc(ops, prec, B, H, cin, cout, k, stride):
+    g = torch.Generator().manual_seed(B * 1000 + H + cin + cout)
+    x = torch.rand(B, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g)
+    pad = k // 2
+    cin_pad = max(cin, 4 if prec == "fp32" else 8)
+    dt = ops.act_dtype(prec)
+    x_nhwc = torch.zeros(B, H, H, cin_pad)
+    x_nhwc[..., :cin] = x.permute(0, 2, 3, 1)
+    x_in = x_nhwc.to(dt)
+    w_ref = w.half().float() if prec == "fp16" else w
+    ref = F.relu(F.conv2d(x_in[..., :cin].float().permute(0, 3, 1, 2), w_ref, b, stride, pad)).permute(0, 2, 3, 1)
+    wp = ops.pack_weight(prec, ops.conv_weight_matrix(w, cin_pad))
+    out = ops.conv2d(prec, x_in.cuda(), wp, cout, k, k, stride, pad, bias=b.cuda(), act="relu")
+    err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
+    tol = TOL[prec] if prec != "fp16" else 2e-3
+    assert err < tol, f"{prec} conv {B}x{H}x{cin}->{cout} k{k}s{stride}: {err:.3e}"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("B,S,heads,masked", [(2, 128, 12, False), (3, 80, 4, True), (2, 197, 16, False),
+                                              (1, 5, 2, False), (2, 64, 2, True)])
+def test_attention(ops, prec, B, S, heads, masked):
+    g = torch.Generator().manual_seed(B * S + heads)
+    D = heads * 64
+    qkv = torch.randn(B * S, 3 * D, generator=g) * 1.5
+    dt = ops.act_dtype(prec)
+    qkv_in = qkv.to(dt)
+    q, k, v = qkv_in.float().view(B, S, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    bias = torch.zeros(B, S)
+    if masked:
+        bias[-1, S // 2:] = torch.finfo(torch.float32).min
+        bias[0, :3] = torch.finfo(torch.float32).min
+    scores = q @ k.transpose(-1, -2) * 0.125 + bias[:, None, None, :]
+    ref = (scores.softmax(-1) @ v).permute(0, 2, 1, 3).reshape(B * S, D)
+    ctx = ops.attention(prec, qkv_in.cuda(), B, S, heads, mask_bias=bias.cuda() if masked else None)
+    err = normalized_max_error(ctx.float().cpu().numpy(), ref.numpy())
+    tol = 1e-5 if prec == "fp32" else 3e-3
+    assert err < tol, f"{prec} attention B{B} S{S} H{heads}: {err:.3e}"
+
+
+def test_attention_fully_masked_row(ops):
+    """A fully masked row is uniform over the keys (finfo.min bias, as HF BERT)."""
+    B, S, heads = 1, 16, 1
+    qkv = torch.randn(B * S, 3 * 64)
+    bias = torch.full((B, S), torch.finfo(torch.float32).min)
+    ctx = ops.attention("fp32", qkv.cuda(), B, S, heads, mask_bias=bias.cuda())
+    v = qkv[:, 128:]
+    np.testing.assert_allclose(ctx.cpu().numpy(), v.mean(0, keepdim=True).expand(S, 64).numpy(), rtol=1e-5,
+                               atol=1e-5)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("rows,D,eps", [(1024, 768, 1e-12), (394, 1024, 1e-6), (3, 64, 1e-5)])
+def test_layernorm(ops, prec, rows, D, eps):
+    g = torch.Generator().manual_seed(rows + D)
+    x = torch.randn(rows, D, generator=g) * 3 + 1
+    gamma = torch.randn(D, generator=g)
+    beta = torch.randn(D, generator=g)
+    ref = F.layer_norm(x, (D,), gamma, beta, eps)
+    yf, yt = ops.layernorm(prec, x.cuda(), gamma.cuda(), beta.cuda(), eps)
+    assert normalized_max_error(yf.cpu().numpy(), ref.numpy()) < 2e-6
+    if prec == "fp16":
+        assert normalized_max_error(yt.float().cpu().numpy(), ref.numpy()) < 1e-3

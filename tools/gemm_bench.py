@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the GEMM / implicit-GEMM conv kernel on model layer shapes.
+
+Times `--reps` back-to-back launches with HIP events on one stream (steady
+state, no host gaps) and prints TFLOP/s per shape.
+"""
+import argparse
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ops = importlib.import_module("starpu-inference-server_amd.ops")
+
+# (name, B, H, Cin, Cout, k, stride)  ResNet-18 bs8 layer shapes (+ stem with Cin padded to 8)
+CONVS = [("stem7x7", 8, 224, 8, 64, 7, 2), ("l1_3x3", 8, 56, 64, 64, 3, 1), ("l2_3x3s2", 8, 56, 64, 128, 3, 2),
+         ("l2_3x3", 8, 28, 128, 128, 3, 1), ("l3_3x3", 8, 14, 256, 256, 3, 1), ("l4_3x3", 8, 7, 512, 512, 3, 1),
+         ("l4_ds1x1", 8, 14, 256, 512, 1, 2)]
+# (name, M, N, K)  BERT-base bs8 S128 / ViT-L bs16
+GEMMS = [("bert_qkv", 1024, 2304, 768), ("bert_out", 1024, 768, 768), ("bert_ff1", 1024, 3072, 768),
+         ("bert_ff2", 1024, 768, 3072), ("vit_qkv", 3152, 3072, 1024), ("vit_ff1", 3152, 4096, 1024),
+         ("vit_ff2", 3152, 1024, 4096), ("sq4096", 4096, 4096, 4096)]
+
+
+def timeit(fn, reps):
+    """Device time per launch: `reps` launches captured in one graph, replayed."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(3):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (3 * reps)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--prec", default="fp16")
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dt = ops.act_dtype(a.prec)
+    ws = ops.workspace()
+    rng = np.random.default_rng(0)
+    for name, B, H, cin, cout, k, st in CONVS:
+        if a.only and a.only not in name:
+            continue
+        x = torch.randn(B, H, H, cin, device="cuda").to(dt)
+        w = rng.standard_normal((cout, k * k * cin)).astype(np.float32) * 0.05
+        wp = ops.pack_weight(a.prec, w)
+        pad = k // 2
+        oh = (H + 2 * pad - k) // st + 1
+        out = torch.empty(B, oh, oh, cout, device="cuda", dtype=dt)
+        ms = timeit(lambda: ops.conv2d(a.prec, x, wp, cout, k, k, st, pad, ws=ws, out=out), a.reps)
+        fl = 2.0 * B * oh * oh * cout * k * k * cin
+        print(f"conv {name:10s} M={B*oh*oh:6d} N={cout:4d} K={k*k*cin:5d}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s")
+    for name, M, N_, K in GEMMS:
+        if a.only and a.only not in name:
+            continue
+        A = torch.randn(M, K, device="cuda").to(dt)
+        w = rng.standard_normal((N_, K)).astype(np.float32) * 0.05
+        wp = ops.pack_weight(a.prec, w)
+        out = torch.empty(M, N_, device="cuda", dtype=torch.float32)
+        ms = timeit(lambda: ops.gemm(a.prec, A, wp, N_, out=out, ws=ws), a.reps)
+        fl = 2.0 * M * N_ * K
+        print(f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
