@@ -58,6 +58,26 @@ def percentile(samples, p):
     return xs[lo] + (xs[hi] - xs[lo]) * (pos - lo)
 
 
+def reduce_max_elapsed(elapsed: float, world: int) -> float:
+    """Max over ranks of the barrier-bracketed timed region (control plane only, gloo)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_requests(n: int, rank: int, world: int) -> list:
+    """Request-level sharding across independent per-GPU workers (no data-path collective):
+    contiguous blocks, as an eager shared queue drained by per-device workers would end up."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return list(range(lo, lo + base + (1 if rank < extra else 0)))
+
+
 def make_inputs(name, batch, rng, seq=128):
     if name.startswith("bert"):
         ids = rng.integers(0, 30522, size=(batch, seq), dtype=np.int64)
@@ -150,11 +170,7 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_max_elapsed(t1 - t0, world)
     task_lat_ms = [s.elapsed_time(e) for step in events for (s, e) in step]
     inferences = world * W * args.batch * args.steps
     value = inferences / elapsed

@@ -88,9 +88,11 @@ class TensorView(C.Structure):
     ]
 
 
+# err is a raw char* the callback writes into (c_void_p: ctypes would hand a
+# c_char_p argument to Python as an immutable bytes copy).
 CPU_FORWARD_FN = C.CFUNCTYPE(
     C.c_int, C.c_void_p, C.POINTER(TensorView), C.c_int, C.POINTER(TensorView), C.c_int,
-    C.c_char_p, C.c_size_t)
+    C.c_void_p, C.c_size_t)
 
 
 class CodeletArgs(C.Structure):

@@ -289,3 +289,11 @@ def build(name: str, seed: int = 0, **kw) -> nn.Module:
     if name not in table:
         raise KeyError(f"unknown model {name!r}; known: {sorted(table)}")
     return table[name](seed=seed, **kw)
+
+
+# TorchScript names a class by its Python module path; this package's directory
+# name is not an identifier, so give the zoo's modules a loadable qualified name
+# (a traced/scripted model must round-trip through .pt like the reference's).
+for _cls in (BasicBlock, Bottleneck, ResNet, MLPBlock, EncoderBlock, Encoder, VisionTransformer, BertWrapper,
+             AddConstant):
+    _cls.__module__ = "spi_zoo"

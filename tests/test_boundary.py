@@ -1,0 +1,273 @@
+"""CPU tests of the C-ABI boundary (no GPU needed).
+
+Mirrors the reference's codelet tests that run without a device:
+buffer_byte_size (src/core/starpu_setup.cpp:515-542), select_gpu_module
+(tests/unit/core/unit_starpu_setup.cpp:4106-4183), the missing-replica error
+(:2435-2472), the CPU codelet over hand-built buffers
+(tests/integration/starpu/integration_starpu_setup.cpp:42-60) and
+copy_output_to_buffer's checks (tests/unit/core/unit_tensor_builder.cpp:159-410).
+"""
+import ctypes as C
+import glob
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    names = set()
+    for path in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        for line in open(path):
+            if line.lstrip().startswith(("typedef", "*", "/*", "#")):
+                continue
+            m = re.match(r"^[A-Za-z_][\w \t\*]*?\b(spi_\w+)\s*\(", line)
+            if m:
+                names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_header_symbol(spi):
+    names = header_functions()
+    assert len(names) >= 36
+    out = subprocess.run(["nm", "-D", "--defined-only", spi._native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = sorted(names - exported)
+    assert not missing, f"declared but not exported: {missing}"
+    for n in names:  # and every one is bound in ctypes
+        assert n in spi._native._PROTOS, n
+
+
+PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "spi_codelet.h"
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+#define S(T) printf(#T " %zu\n", sizeof(T));
+int main(void) {
+  S(spi_vector_interface) F(spi_vector_interface, ptr) F(spi_vector_interface, nx)
+  F(spi_vector_interface, elemsize) F(spi_vector_interface, allocsize)
+  S(spi_variable_interface) F(spi_variable_interface, ptr) F(spi_variable_interface, elemsize)
+  S(spi_tensor_view) S(spi_named_tensor) S(spi_model_config)
+  S(spi_codelet_args) F(spi_codelet_args, dims) F(spi_codelet_args, input_types)
+  F(spi_codelet_args, output_types) F(spi_codelet_args, model_cpu) F(spi_codelet_args, cpu_forward)
+  F(spi_codelet_args, device_ids) F(spi_codelet_args, models_gpu) F(spi_codelet_args, codelet_start_ns)
+  F(spi_codelet_args, executed_on) F(spi_codelet_args, status) F(spi_codelet_args, error)
+  return 0;
+}
+"""
+
+
+def test_ctypes_layouts_match_the_c_header(spi, tmp_path):
+    src = tmp_path / "probe.c"
+    src.write_text(PROBE)
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                             check=True).stdout.splitlines())
+    N = spi._native
+    types = {"spi_vector_interface": N.VectorInterface, "spi_variable_interface": N.VariableInterface,
+             "spi_tensor_view": N.TensorView, "spi_named_tensor": N.NamedTensor, "spi_model_config": N.ModelConfig,
+             "spi_codelet_args": N.CodeletArgs}
+    for key, val in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            assert getattr(types[t], f).offset == int(val), key
+        else:
+            assert C.sizeof(types[key]) == int(val), key
+
+
+def test_buffer_byte_size(spi):
+    N = spi._native
+    var = spi.make_variable_interface(0x1000, 12)
+    assert spi.buffer_byte_size(var) == 12
+    vec = spi.make_vector_interface(0x1000, 5, 8)
+    assert spi.buffer_byte_size(vec) == 40
+    vec.nx = 0
+    assert spi.buffer_byte_size(vec) == 0
+    bad = N.VariableInterface(3, 0, 0, 0, 4)  # CSR id: unsupported
+    with pytest.raises(spi.InferenceExecutionException, match="Unsupported StarPU buffer interface id 3"):
+        spi.buffer_byte_size(bad)
+    with pytest.raises(spi.InferenceExecutionException, match="buffer is null"):
+        spi.buffer_byte_size(None)
+
+
+@pytest.fixture(scope="module")
+def fake_replicas(spi):
+    # host-only replicas (device -1): valid spi_model handles without a GPU
+    return [spi.ModelReplica(None, -1, "fp32", family="affine") for _ in range(2)]
+
+
+def test_select_replica_mappings(spi, fake_replicas):
+    r0, r1 = fake_replicas
+    p = spi.InferenceParams(models_gpu=[r0])
+    assert spi.select_gpu_module(p, worker_id=3, device_id=0) == 0          # index = device id
+    p = spi.InferenceParams(models_gpu=[r0, r1], device_ids=[0, 2])
+    assert spi.select_gpu_module(p, worker_id=5, device_id=2) == 1          # device id mapping
+    p = spi.InferenceParams(models_gpu=[r0, r1], device_ids=[0, 0], worker_ids=[7, 9])
+    assert spi.select_gpu_module(p, worker_id=9, device_id=0) == 1          # worker id mapping
+    p = spi.InferenceParams(models_gpu=[r0], device_ids=[0], worker_ids=[7])
+    with pytest.raises(spi.StarPUCodeletException, match="No GPU model replica available for worker 8 on device 0"):
+        spi.select_gpu_module(p, worker_id=8, device_id=0)
+    p = spi.InferenceParams(models_gpu=[None])
+    with pytest.raises(spi.StarPUCodeletException, match="No GPU model replica available for device 0"):
+        spi.select_gpu_module(p, worker_id=0, device_id=0)
+
+
+def test_hip_codelet_without_replica_raises(spi):
+    """unit_starpu_setup.cpp:2435-2472: no replica -> StarPUCodeletException (no device touched)."""
+    params = spi.InferenceParams(num_inputs=0, num_outputs=0)
+    with spi.worker_context(91, 0, None):
+        with pytest.raises(spi.StarPUCodeletException, match=r"Codelet failure: \[ERROR\] No GPU model replica"):
+            spi.InferenceCodelet.hip_inference_func(None, params)
+
+
+def test_abi_version_mismatch_is_rejected(spi, fake_replicas):
+    a = spi.InferenceParams(models_gpu=[fake_replicas[0]]).to_args()
+    a.abi_version = 99
+    with pytest.raises(spi.StarPUCodeletException, match="ABI version"):
+        spi.InferenceCodelet.hip_inference_func(None, a)
+
+
+def _cpu_call(spi, module, x, out, n_out=1):
+    params = spi.make_params([list(x.shape)], [x.dtype], num_outputs=n_out,
+                             model_cpu=spi.TorchCpuForward(module), output_types=[out.dtype] * n_out)
+    bufs = [spi.make_variable_interface(x.data_ptr(), x.numel() * x.element_size()),
+            spi.make_variable_interface(out.data_ptr(), out.numel() * out.element_size())]
+    with spi.worker_context(4, -1, None):
+        return spi.InferenceCodelet.cpu_inference_func(bufs, params)
+
+
+def test_cpu_codelet_x_plus_one(spi, zoo):
+    """integration_starpu_setup.cpp:42-60: x+1 on {1,2,3} -> {2,3,4}, executed_on CPU, stamps ordered."""
+    x = torch.tensor([1.0, 2.0, 3.0])
+    out = torch.zeros(3)
+    import time
+    before = time.monotonic_ns()
+    args = _cpu_call(spi, zoo.AddConstant(1.0), x, out)
+    after = time.monotonic_ns()
+    assert out.tolist() == [2.0, 3.0, 4.0]
+    assert args.executed_on == spi._native.DEVICE_CPU and args.worker_id == 4
+    assert before <= args.codelet_start_ns <= args.inference_start_ns <= args.codelet_end_ns <= after
+
+
+def test_cpu_codelet_output_checks(spi, zoo):
+    x = torch.tensor([1.0, 2.0, 3.0])
+    with pytest.raises(spi.StarPUCodeletException, match="Output buffer size mismatch"):
+        _cpu_call(spi, zoo.AddConstant(1.0), x, torch.zeros(4))
+
+    class Pair(torch.nn.Module):
+        def forward(self, t):
+            return t, t + 1
+
+    with pytest.raises(spi.StarPUCodeletException, match="Mismatch between model outputs and StarPU buffers"):
+        _cpu_call(spi, Pair(), x, torch.zeros(3))
+
+    class Const(torch.nn.Module):
+        def forward(self, t):
+            return 5
+
+    with pytest.raises(spi.StarPUCodeletException, match="Unsupported model output type"):
+        _cpu_call(spi, Const(), x, torch.zeros(3))
+    with pytest.raises(spi.StarPUCodeletException, match="Output type mismatch"):
+        _cpu_call(spi, zoo.AddConstant(1.0), x, torch.zeros(3, dtype=torch.float64))
+
+
+def test_cpu_codelet_without_model(spi):
+    x = torch.ones(2)
+    params = spi.make_params([[2]], [torch.float32])
+    bufs = [spi.make_variable_interface(x.data_ptr(), 8), spi.make_variable_interface(x.data_ptr(), 8)]
+    with pytest.raises(spi.StarPUCodeletException, match="No CPU model"):
+        spi.InferenceCodelet.cpu_inference_func(bufs, params)
+
+
+def test_layout_limits(spi, zoo):
+    x = torch.ones(2)
+    params = spi.make_params([[2]], [torch.float32], model_cpu=spi.TorchCpuForward(zoo.AddConstant(1.0)))
+    params.max_inputs = 0
+    bufs = [spi.make_variable_interface(x.data_ptr(), 8), spi.make_variable_interface(x.data_ptr(), 8)]
+    with pytest.raises(spi.StarPUCodeletException, match="Too many input tensors"):
+        spi.InferenceCodelet.cpu_inference_func(bufs, params)
+
+
+def test_codelet_descriptor(spi):
+    """InferenceCodelet ctor (starpu_setup.cpp:559-568): variable buffers, FORKJOIN, async GPU func."""
+    cl = spi.InferenceCodelet()
+    assert cl.nbuffers == -1 and cl.type == "STARPU_FORKJOIN" and cl.hip_flags == 1
+    assert cl.cpu_funcs[0] == cl.cpu_inference_func and cl.hip_funcs[0] == cl.hip_inference_func
+    # without <starpu.h> the C adapter reports itself unavailable rather than guessing the struct
+    assert spi.lib.spi_codelet_init(None) == spi._native.SPI_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("name,kw,gflop", [
+    ("resnet18", {}, 3.628), ("resnet152", {}, 23.027), ("bert_base", {"seq_len": 128}, 22.35),
+    ("vit_l_16", {}, 123.1)])
+def test_host_replica_recognition_and_flops(spi, zoo, name, kw, gflop):
+    """Recogniser + packer on the full architectures (host-only replica); FLOPs match SURVEY.md 8(d)."""
+    m = zoo.build(name)
+    r = spi.ModelReplica(m, -1, "fp16", max_batch=2, **kw)
+    assert abs(r.flops(1) / 1e9 - gflop) / gflop < 2e-3
+    assert r.weight_bytes > 0
+    r16x3 = spi.ModelReplica(m, -1, "fp16x3", max_batch=2, **kw)
+    assert "f16x3" in r16x3.description
+
+
+def test_flops_match_torch_flop_counter(spi, zoo):
+    from torch.utils.flop_counter import FlopCounterMode
+    m = zoo.resnet18(image=64)
+    with FlopCounterMode(display=False) as fc:
+        m(torch.rand(2, 3, 64, 64))
+    r = spi.ModelReplica(m, -1, "fp32", max_batch=2, image_size=64)
+    assert abs(r.flops(2) - fc.get_total_flops()) / fc.get_total_flops() < 1e-6
+
+
+def test_recognition_errors(spi, zoo):
+    m = zoo.resnet18(image=64)
+    sd = {k: v for k, v in m.state_dict().items() if "layer3.0.conv2" not in k}
+    holder = torch.nn.Module()
+    for k, v in sd.items():
+        holder.register_buffer(k.replace(".", "__"), v)
+
+    class Named(torch.nn.Module):
+        def __init__(self, d):
+            super().__init__()
+            self.d = d
+
+        def named_parameters(self, *a, **k):
+            return iter([])
+
+        def named_buffers(self, *a, **k):
+            return iter(self.d.items())
+
+    with pytest.raises(spi.InferenceExecutionException, match="missing parameter 'layer3.0.conv2.weight'"):
+        spi.ModelReplica(Named(sd), -1, "fp16", image_size=64)
+    with pytest.raises(spi.InferenceExecutionException, match="unrecognised model"):
+        spi.ModelReplica(Named({"foo.weight": torch.zeros(2)}), -1, "fp16")
+
+
+def test_torchscript_file_is_accepted(spi, zoo, tmp_path):
+    """The reference's on-disk format: a traced TorchScript .pt (models/import_resnet.py)."""
+    m = zoo.resnet18(image=64)
+    path = str(tmp_path / "resnet18.pt")
+    torch.jit.trace(m, torch.rand(1, 3, 64, 64)).save(path)
+    r_file = spi.ModelReplica(path, -1, "fp16", image_size=64)
+    r_mod = spi.ModelReplica(m, -1, "fp16", image_size=64)
+    assert r_file.description == r_mod.description and r_file.weight_bytes == r_mod.weight_bytes
+
+
+def test_no_fallback_when_library_missing(tmp_path):
+    """Importing the package without the native library fails loudly."""
+    import shutil
+    import sys
+    pkg = os.path.join(ROOT, "starpu-inference-server_amd")
+    dst = tmp_path / "starpu-inference-server_amd"
+    shutil.copytree(pkg, dst, ignore=shutil.ignore_patterns("*.so", "csrc", "__pycache__"))
+    code = "import importlib, sys; sys.path.insert(0, %r); importlib.import_module('starpu-inference-server_amd')"
+    r = subprocess.run([sys.executable, "-c", code % str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode != 0 and "libspi_hip.so is missing" in r.stderr

@@ -1,0 +1,64 @@
+"""Host-side logic: latency statistics, bench contract helpers, multi-rank control (gloo)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_percentile_matches_reference_definition():
+    """latency_statistics.hpp:52-93: sort, p<=0 -> min, p>=100 -> max, else lerp at p/100*(n-1)."""
+    xs = [5.0, 1.0, 3.0, 2.0, 4.0]
+    assert bench.percentile(xs, 0) == 1.0 and bench.percentile(xs, 100) == 5.0
+    assert bench.percentile(xs, 50) == 3.0
+    assert bench.percentile([1.0, 2.0], 50) == 1.5
+    assert abs(bench.percentile(list(range(101)), 95) - 95.0) < 1e-12
+    assert bench.percentile([7.0], 85) == 7.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    elapsed = bench.reduce_max_elapsed(0.5 + rank, world)
+    shard = bench.shard_requests(100, rank, world)
+    q.put((rank, elapsed, shard))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_max_time_and_request_sharding():
+    """The N>1 bench path: barrier-bracketed timing reduced by MAX; requests sharded with no collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(abs(e - 1.5) < 1e-12 for _, e, _ in res)
+    shards = [s for _, _, s in res]
+    assert shards[0] + shards[1] == list(range(100))
+
+
+def test_shard_requests_is_a_partition():
+    for world in (1, 2, 3, 8):
+        got = sorted(i for r in range(world) for i in bench.shard_requests(37, r, world))
+        assert got == list(range(37))

@@ -152,3 +152,33 @@ def test_affine_codelet_like_reference(spi, gpu):
     assert out.cpu().tolist() == [2.5, 3.5, 4.5]
     assert args.device_id == 0 and args.worker_id == 77 and args.executed_on == 2
     assert args.codelet_start_ns > 0 and args.codelet_end_ns >= args.codelet_start_ns
+
+
+GOLDEN_FIXTURES = ["resnet18_img64_b2", "resnet_bottleneck_1221_img64_b2", "bert_L2_S16_b2_masked",
+                   "vit_img32_p16_L2_D128_b2"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_FIXTURES)
+@pytest.mark.parametrize("prec", ["fp32", "fp16x3", "fp16"])
+def test_hip_matches_committed_golden_fixtures(spi, gpu, name, prec):
+    """HIP codelet vs the committed CPU-oracle fixtures (tests/golden/make_golden.py)."""
+    import importlib
+    import os
+    import sys
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, golden)
+    mk = importlib.import_module("make_golden")
+    g = np.load(os.path.join(golden, "models.npz"))
+    model, _ = mk.SMALL[name]()
+    inputs = [g[f"{name}__in{i}"] for i in range(2) if f"{name}__in{i}" in g]
+    ref = g[f"{name}__out"]
+    if name.startswith("bert") and prec == "fp16x3":
+        pytest.skip("transformer families run fp32 or fp16")
+    kw = {"image_size": inputs[0].shape[-1]} if inputs[0].ndim == 4 else {"seq_len": 128}
+    rep = spi.ModelReplica(model, 0, prec if not (name.startswith("vit") and prec == "fp16x3") else "fp32",
+                           max_batch=2, **kw)
+    got = hip_forward(spi, rep, inputs, ref.shape)
+    err = normalized_max_error(got, ref)
+    tol = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 1e-2}[prec]
+    print(f"golden {name} {prec} err={err:.3e}")
+    assert err < tol
