@@ -81,20 +81,27 @@ __device__ __forceinline__ float apply_act(float v, Act act) {
 }
 
 template <int MODE>
-__device__ __forceinline__ void epilogue_store(const KArgs& a, int m, int n, float v) {
+__device__ __forceinline__ float load_res(const KArgs& a, int m, int n) {
   using Out = typename Traits<MODE>::Out;
-  const GemmDesc& d = a.d;
-  if (a.p.bias) v += a.p.bias[n];
-  if (a.p.res) {
-    const size_t idx = (size_t)m * d.ldr + n;
-    v += d.res_f32 ? static_cast<const float*>(a.p.res)[idx]
-                   : static_cast<float>(static_cast<const Out*>(a.p.res)[idx]);
-  }
-  v = apply_act(v, d.act);
-  if (d.out_f32)
-    static_cast<float*>(a.p.C)[(size_t)m * d.ldc + n] = v;
+  const size_t idx = (size_t)m * a.d.ldr + n;
+  return a.d.res_f32 ? static_cast<const float*>(a.p.res)[idx]
+                     : static_cast<float>(static_cast<const Out*>(a.p.res)[idx]);
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_out(const KArgs& a, int m, int n, float v) {
+  using Out = typename Traits<MODE>::Out;
+  if (a.d.out_f32)
+    static_cast<float*>(a.p.C)[(size_t)m * a.d.ldc + n] = v;
   else
-    static_cast<Out*>(a.p.C)[(size_t)m * d.ldc + n] = static_cast<Out>(v);
+    static_cast<Out*>(a.p.C)[(size_t)m * a.d.ldc + n] = static_cast<Out>(v);
+}
+
+template <int MODE>
+__device__ __forceinline__ void epilogue_store(const KArgs& a, int m, int n, float v) {
+  if (a.p.bias) v += a.p.bias[n];
+  if (a.p.res) v += load_res<MODE>(a, m, n);
+  store_out<MODE>(a, m, n, apply_act(v, a.d.act));
 }
 
 __device__ __forceinline__ void split8(const u32x4& x0, const u32x4& x1, half8& hi, half8& lo) {
@@ -255,9 +262,38 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) issue(s, s);
 
+  // Epilogue operands fetched now so their latency hides under the K loop
+  // (single-slice tiles only; the split-K reducer reads them itself).
+  // Only small tiles (16 accumulators per lane) can spare the registers.
+  constexpr bool kPrefetch = TI * TJ <= 4;
+  const bool pre = kPrefetch && gridDim.y == 1;
+  float rpre[TI][TJ][4], bpre[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int n = n0 + wn * WTN + j * 16 + fr;
+    bpre[j] = (pre && a.p.bias && n < d.N) ? a.p.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+        const int n = n0 + wn * WTN + j * 16 + fr;
+        rpre[i][j][r] = (pre && a.p.res && m < d.M && n < d.N) ? load_res<MODE>(a, m, n) : 0.f;
+      }
+
   for (int t = 0; t < nsteps; ++t) {
     // Step t has landed once at most (issued steps after t) DMA groups remain.
-    if constexpr (STAGES == 3) {
+    if constexpr (STAGES == 4) {
+      if (t + 2 < nsteps)
+        dma_wait_barrier<2 * QPS>();
+      else if (t + 1 < nsteps)
+        dma_wait_barrier<QPS>();
+      else
+        dma_wait_barrier<0>();
+    } else if constexpr (STAGES == 3) {
       if (t + 1 < nsteps)
         dma_wait_barrier<QPS>();
       else
@@ -345,7 +381,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
           const int n = n0 + wn * WTN + j * 16 + fr;
-          if (m < d.M && n < d.N) epilogue_store<MODE>(a, m, n, acc[i][j][r]);
+          if (m < d.M && n < d.N) {
+            if constexpr (kPrefetch)
+              store_out<MODE>(a, m, n, apply_act(acc[i][j][r] + bpre[j] + rpre[i][j][r], d.act));
+            else
+              epilogue_store<MODE>(a, m, n, acc[i][j][r]);
+          }
         }
     return;
   }
@@ -419,28 +460,50 @@ struct Plan {
 
 int estep_of(Prec prec) { return prec == Prec::F16 ? 64 : 32; }
 
+// Tuning hook: SPI_GEMM_PLAN="bm,bn,stages,splits" forces the plan (micro-benchmarks only).
+bool plan_override(Plan* pl) {
+  static const char* env = std::getenv("SPI_GEMM_PLAN");
+  if (!env || !*env) return false;
+  int bm = 0, bn = 0, st = 0, sp = 0;
+  if (std::sscanf(env, "%d,%d,%d,%d", &bm, &bn, &st, &sp) != 4) return false;
+  const bool ok_tile = (bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64);
+  const bool ok_st = st >= 2 && st <= 4 && !(bm == 128 && bn == 128 && st > 2) && !(bm == 128 && bn == 64 && st > 3);
+  if (!ok_tile || !ok_st || sp < 1) return false;
+  *pl = Plan{bm, bn, st, sp, 0};
+  return true;
+}
+
 Plan choose_plan(const GemmDesc& d, Prec prec) {
   constexpr int kTarget = 256;  // CUs
   const int ES = estep_of(prec);
+  const int ksteps = d.Kpad / ES;
+  Plan forced;
+  if (plan_override(&forced)) {
+    const int sp = std::min(forced.splits, ksteps);
+    const int kt_per = (ksteps + sp - 1) / sp;
+    forced.k_per_split = kt_per * ES;
+    forced.splits = (ksteps + kt_per - 1) / kt_per;
+    return forced;
+  }
   static const int cfg[3][2] = {{128, 128}, {128, 64}, {64, 64}};
-  Plan pl{64, 64, 3, 1, d.Kpad};
+  Plan pl{64, 64, 2, 1, d.Kpad};
   for (auto& c : cfg) {
     if (c[1] == 128 && d.N <= 64) continue;
     const int tiles = ((d.M + c[0] - 1) / c[0]) * ((d.N + c[1] - 1) / c[1]);
     if (tiles >= kTarget) {
       pl.bm = c[0];
       pl.bn = c[1];
-      pl.stages = (c[0] == 128 && c[1] == 128) ? 2 : 3;
+      pl.stages = (c[0] == 128 && c[1] == 128) ? 2 : (c[0] == 64 && ksteps < 16 ? 2 : 3);
       return pl;
     }
   }
   const int tiles = ((d.M + 63) / 64) * ((d.N + 63) / 64);
-  const int ksteps = d.Kpad / ES;
   int splits = 1;
   if (tiles < kTarget / 2 && ksteps >= 6) splits = std::max(1, std::min(ksteps / 3, (2 * kTarget + tiles - 1) / tiles));
   const int kt_per = (ksteps + splits - 1) / splits;
   pl.k_per_split = kt_per * ES;
   pl.splits = (ksteps + kt_per - 1) / kt_per;
+  pl.stages = kt_per >= 16 ? 3 : 2;  // a deeper ring pays only on long K loops
   return pl;
 }
 
@@ -473,8 +536,14 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   const dim3 grid(a.tiles, pl.splits);
   if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(a, grid, s);
+  else if (pl.bm == 128 && pl.stages == 2)
+    launch_tile<MODE, 128, 64, 2>(a, grid, s);
   else if (pl.bm == 128)
     launch_tile<MODE, 128, 64, 3>(a, grid, s);
+  else if (pl.stages == 2)
+    launch_tile<MODE, 64, 64, 2>(a, grid, s);
+  else if (pl.stages == 4)
+    launch_tile<MODE, 64, 64, 4>(a, grid, s);
   else
     launch_tile<MODE, 64, 64, 3>(a, grid, s);
 }

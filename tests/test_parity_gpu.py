@@ -172,11 +172,8 @@ def test_hip_matches_committed_golden_fixtures(spi, gpu, name, prec):
     model, _ = mk.SMALL[name]()
     inputs = [g[f"{name}__in{i}"] for i in range(2) if f"{name}__in{i}" in g]
     ref = g[f"{name}__out"]
-    if name.startswith("bert") and prec == "fp16x3":
-        pytest.skip("transformer families run fp32 or fp16")
     kw = {"image_size": inputs[0].shape[-1]} if inputs[0].ndim == 4 else {"seq_len": 128}
-    rep = spi.ModelReplica(model, 0, prec if not (name.startswith("vit") and prec == "fp16x3") else "fp32",
-                           max_batch=2, **kw)
+    rep = spi.ModelReplica(model, 0, prec, max_batch=2, **kw)
     got = hip_forward(spi, rep, inputs, ref.shape)
     err = normalized_max_error(got, ref)
     tol = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 1e-2}[prec]
