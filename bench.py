@@ -1,23 +1,26 @@
 #!/usr/bin/env python3
 """MI355X inference-codelet benchmark (BASELINE.json metric: inferences/sec + p50 latency).
 
-A *step* is one task per worker: each of the `--workers` workers of a GPU
-(StarPU's STARPU_NWORKER_PER_CUDA=4 analogue, models/resnet18.yml:6) calls the
-HIP codelet (libspi_hip.so, through the C-ABI) on its own HIP stream over one
-synthetic batch already resident in HBM.  Default workload = BASELINE.json
-configs[1]: ResNet-18, batch 8, fp16 MFMA, one MI355X.
+Headline workload = BASELINE.json configs[1]: ResNet-18, batch 8 per task, fp16
+MFMA, one MI355X -- run in the parity-grade fp16x3 mode (split-fp16 MFMA,
+fp32-grade results; plain fp16 operands miss the 1e-3 bar on this network,
+DESIGN.md 3).  A *step* is one task per worker: each of the `--workers` workers
+of a GPU (STARPU_NWORKER_PER_CUDA=4, models/resnet18.yml:6) calls the HIP
+codelet (libspi_hip.so, through the C-ABI) on its own HIP stream over one
+synthetic batch already resident in HBM.
 
-Multi-GPU: one process per GPU (torch.distributed.run), one weight replica
-per device, tasks sharded across devices with no data-path collective
+Multi-GPU: one process per GPU (torch.distributed.run), one weight replica per
+device, tasks sharded across devices with no data-path collective
 ("scaling": "weak"); a gloo barrier brackets the timed region and the time is
-the max over ranks.  `value` = inferences of all ranks / that time.
+the max over ranks; `value` = inferences of all ranks / that time.
 
-Also reported: p50 per-task device latency (HIP events on the worker stream,
-linear-interpolated percentile as src/core/latency_statistics.hpp:52-93), p50
-end-to-end latency including pinned H2D + D2H (serial, one task in flight),
-the dominant kernel's roofline (HIP events on its launch stream) and the CPU
-codelet baseline (oracle: ATen CPU forward of the same TorchScript-able module,
-rank 0 only, bounded sample).
+Also reported (rank 0): p50 per-task device latency (hipEvents on the worker
+stream, linear-interpolated percentile as src/core/latency_statistics.hpp:52-93),
+p50 end-to-end latency including pinned H2D + D2H, the dominant kernel's
+roofline (hipEvents on its launch stream), the CPU codelet baseline (oracle =
+ATen CPU forward of the same module, bounded sample) and, single-GPU only,
+extras: plain-fp16 throughput, BERT-base seq128 bs8, ResNet-18 bs1 latency and
+the PCIe-inclusive mini-runtime path.
 """
 from __future__ import annotations
 
@@ -38,11 +41,10 @@ BASELINE_METRIC = "inferences/sec + p50 latency, ResNet-18 bs=1 & BERT-base seq=
 WORKLOADS = {
     "resnet18": "ResNet-18 bs=8 fp16, single MI355X HIP codelet (conv-as-implicit-GEMM MFMA)",
     "bert_base": "bert-base-uncased seq=128 bs=8 fp16, 1xMI355X (QKV GEMM + softmax + LayerNorm fused)",
-    "resnet152": "ResNet-152 bs=32 fp16, StarPU-style HIP workers per MI355X (request-parallel, no RCCL)",
+    "resnet152": "ResNet-152 bs=32 fp16, HIP workers per MI355X (request-parallel, no RCCL)",
     "vit_l_16": "ViT-L/16 224^2 bs=16 fp16 (patch-embed GEMM + MFMA attention, LDS-tiled)",
 }
 PEAK_TFLOPS = {"fp16": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
-PEAK_HBM_GBS = 8000.0
 
 
 def percentile(samples, p):
@@ -86,6 +88,135 @@ def make_inputs(name, batch, rng, seq=128):
     return [rng.random((batch, 3, 224, 224), dtype=np.float32)], (batch, 1000)
 
 
+class Harness:
+    """Prebuilt codelet calls (cl_arg + buffers + stream) for `workers` workers of one device."""
+
+    def __init__(self, spi, replica, name, dev, batch, workers, rng):
+        import torch
+
+        self.spi, self.lib, self.N = spi, spi.lib, spi._native
+        self.torch = torch
+        self.dev = dev
+        self.replica = replica
+        self.batch = batch
+        self.streams = [torch.cuda.Stream(dev) for _ in range(workers)]
+        self.host_inputs, self.out_shape = make_inputs(name, batch, rng)
+        self.d_in = [[torch.from_numpy(x).to(dev) for x in self.host_inputs] for _ in range(workers)]
+        self.d_out = [torch.empty(self.out_shape, device=dev, dtype=torch.float32) for _ in range(workers)]
+        torch.cuda.synchronize(dev)
+        self.calls = []
+        for w in range(workers):
+            params = spi.make_params([list(x.shape) for x in self.d_in[w]], [x.dtype for x in self.d_in[w]],
+                                     models_gpu=[replica], device_ids=[dev])
+            bufs = spi.buffer_array([spi.tensor_interface(x) for x in self.d_in[w]] +
+                                    [spi.tensor_interface(self.d_out[w])])
+            self.calls.append((params.to_args(), bufs, self.streams[w]))
+
+    def task(self, w, ev=None):
+        a, bufs, st = self.calls[w]
+        self.lib.spi_set_worker_context(w, self.dev, C.c_void_p(st.cuda_stream))
+        if ev is not None:
+            ev[0].record(st)
+        self.lib.spi_hip_inference_func(bufs, C.byref(a))
+        if ev is not None:
+            ev[1].record(st)
+        if a.status != self.N.SPI_OK:
+            raise RuntimeError(a.error.decode())
+
+    def throughput(self, steps, warmup, world=1, dist=None):
+        torch = self.torch
+        W = len(self.calls)
+        for _ in range(warmup):
+            for w in range(W):
+                self.task(w)
+        torch.cuda.synchronize(self.dev)
+        events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(W)]
+                  for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            for w in range(W):
+                self.task(w, events[k][w])
+        torch.cuda.synchronize(self.dev)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = reduce_max_elapsed(t1 - t0, world)
+        lat = [s.elapsed_time(e) for step in events for (s, e) in step]
+        return elapsed, lat
+
+    def serial_e2e(self, iters):
+        """pinned host -> H2D -> codelet -> D2H -> sync, one task in flight."""
+        torch = self.torch
+        st = self.streams[0]
+        pinned_in = [torch.from_numpy(x).pin_memory() for x in self.host_inputs]
+        pinned_out = torch.empty(self.out_shape, dtype=torch.float32).pin_memory()
+        out = []
+        for i in range(iters + 3):
+            ts = time.perf_counter()
+            with torch.cuda.stream(st):
+                for h, d in zip(pinned_in, self.d_in[0]):
+                    d.copy_(h, non_blocking=True)
+                self.task(0)
+                pinned_out.copy_(self.d_out[0], non_blocking=True)
+            st.synchronize()
+            if i >= 3:
+                out.append((time.perf_counter() - ts) * 1e3)
+        return out
+
+    def dominant_kernel(self, precision):
+        ops = self.replica.profile(self.d_in[0], self.d_out[0], self.streams[0].cuda_stream)
+        totals = {}
+        for op in ops:
+            t = totals.setdefault(op["name"], [0.0, 0, op["flops"], op["bytes"]])
+            t[0] += op["ms"]
+            t[1] += 1
+        name, (tot, cnt, flops, _bytes) = max(totals.items(), key=lambda kv: kv[1][0])
+        ms = tot / cnt
+        peak = PEAK_TFLOPS[precision]
+        ach = flops / (ms * 1e-3) / 1e12
+        fwd_ms = sum(o["ms"] for o in ops)
+        fwd_flops = sum(o["flops"] for o in ops)
+        return {"bound": "mfma", "kernel": name, "launches_per_forward": cnt, "achieved": round(ach, 3),
+                "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 5), "traffic": None,
+                "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(ms, 5),
+                "forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5)}
+
+
+def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4):
+    """Closed loop through the mini-runtime (host buffers, pinned slots, H2D/D2H):
+    inf/s = inferences / (last response - first request) (inference_client.cpp:259-270)."""
+    rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
+    host_inputs, out_shape = make_inputs(name, batch, np.random.default_rng(7))
+    if name.startswith("bert"):
+        in_specs = [((x.shape[1],), np.int64) for x in host_inputs]
+    else:
+        in_specs = [((3, 224, 224), np.float32)]
+    out_elems = int(np.prod(out_shape[1:]))
+    rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers)
+    outs = [np.empty(out_shape, np.float32) for _ in range(inflight)]
+    submitted = 0
+    t0 = time.perf_counter()
+    while submitted < requests:
+        done = len(rt.completions)
+        while submitted < requests and submitted - done < inflight:
+            rt.submit(submitted, host_inputs, [outs[submitted % inflight]])
+            submitted += 1
+        time.sleep(0.0002)
+    rt.drain()
+    first = min(c.submit_ns for c in rt.completions)
+    last = max(c.complete_ns for c in rt.completions)
+    lat = [c.latency_ms for c in rt.completions]
+    ok, failed = rt.stats()
+    rt.close()
+    return {"value": round(requests * batch / ((last - first) * 1e-9), 2), "unit": "inferences/s",
+            "p50_latency_ms": round(percentile(lat, 50), 4), "p95_latency_ms": round(percentile(lat, 95), 4),
+            "requests": requests, "batch": batch, "inflight": inflight, "workers": workers, "failed": failed,
+            "wall_s": round(time.perf_counter() - t0, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,11 +224,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet18", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp16x3", "fp32"])
+    ap.add_argument("--precision", default="fp16x3", choices=["fp16", "fp16x3", "fp32"])
     ap.add_argument("--workers", type=int, default=4, help="worker streams per GPU")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--latency-iters", type=int, default=40)
+    ap.add_argument("--extras", type=int, default=1, help="single-GPU extra measurements (0 = skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -109,8 +241,6 @@ def main():
 
     spi = importlib.import_module("starpu-inference-server_amd")
     zoo = importlib.import_module("starpu-inference-server_amd.zoo")
-    N = spi._native
-    lib = spi.lib
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -118,93 +248,13 @@ def main():
     dev = local_rank
     torch.cuda.set_device(dev)
 
-    model = zoo.build(args.model, seed=0)
     seq = 128
+    model = zoo.build(args.model, seed=0)
     replica = spi.ModelReplica(model, dev, args.precision, max_batch=args.batch,
-                               seq_len=seq if args.model.startswith("bert") else 0)
-    replica.set_graphs(bool(args.graphs))
-
-    rng = np.random.default_rng(rank)
-    W = args.workers
-    streams = [torch.cuda.Stream(dev) for _ in range(W)]
-    host_inputs, out_shape = make_inputs(args.model, args.batch, rng, seq)
-    d_in = [[torch.from_numpy(x).to(dev) for x in host_inputs] for _ in range(W)]
-    d_out = [torch.empty(out_shape, device=dev, dtype=torch.float32) for _ in range(W)]
-    torch.cuda.synchronize(dev)
-
-    # Prebuilt codelet arguments per worker (the task's cl_arg + buffers).
-    calls = []
-    for w in range(W):
-        params = spi.make_params([list(x.shape) for x in d_in[w]], [x.dtype for x in d_in[w]],
-                                 models_gpu=[replica], device_ids=[dev])
-        a = params.to_args()
-        bufs = spi.buffer_array([spi.tensor_interface(x) for x in d_in[w]] + [spi.tensor_interface(d_out[w])])
-        calls.append((a, bufs, streams[w]))
-
-    def run_task(w, ev=None):
-        a, bufs, st = calls[w]
-        lib.spi_set_worker_context(w, dev, C.c_void_p(st.cuda_stream))
-        if ev is not None:
-            ev[0].record(st)
-        lib.spi_hip_inference_func(bufs, C.byref(a))
-        if ev is not None:
-            ev[1].record(st)
-        if a.status != N.SPI_OK:
-            raise RuntimeError(a.error.decode())
-
-    for _ in range(args.warmup):
-        for w in range(W):
-            run_task(w)
-    torch.cuda.synchronize(dev)
-
-    events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(W)]
-              for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        for w in range(W):
-            run_task(w, events[k][w])
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = reduce_max_elapsed(t1 - t0, world)
-    task_lat_ms = [s.elapsed_time(e) for step in events for (s, e) in step]
-    inferences = world * W * args.batch * args.steps
-    value = inferences / elapsed
-    ms_per_step = elapsed * 1e3 / args.steps
-
-    # Serial end-to-end latency: pinned host -> H2D -> codelet -> D2H, one task in flight.
-    st0 = streams[0]
-    pinned_in = [torch.from_numpy(x).pin_memory() for x in host_inputs]
-    pinned_out = torch.empty(out_shape, dtype=torch.float32).pin_memory()
-    e2e = []
-    for i in range(args.latency_iters + 3):
-        ts = time.perf_counter()
-        with torch.cuda.stream(st0):
-            for hsrc, dst in zip(pinned_in, d_in[0]):
-                dst.copy_(hsrc, non_blocking=True)
-            run_task(0)
-            pinned_out.copy_(d_out[0], non_blocking=True)
-        st0.synchronize()
-        if i >= 3:
-            e2e.append((time.perf_counter() - ts) * 1e3)
-
-    # Dominant kernel (per-op HIP events on the launch stream, same workload).
-    ops = replica.profile(d_in[0], d_out[0], st0.cuda_stream)
-    totals = {}
-    for op in ops:
-        t = totals.setdefault(op["name"], [0.0, 0, op["flops"], op["bytes"]])
-        t[0] += op["ms"]
-        t[1] += 1
-    dom_name, (dom_ms_total, dom_count, dom_flops, dom_bytes) = max(totals.items(), key=lambda kv: kv[1][0])
-    dom_ms = dom_ms_total / dom_count
-    fwd_ms = sum(op["ms"] for op in ops)
-    fwd_flops = sum(op["flops"] for op in ops)
-    achieved_tf = dom_flops / (dom_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.precision]
+                               seq_len=seq if args.model.startswith("bert") else 0, graphs=bool(args.graphs))
+    h = Harness(spi, replica, args.model, dev, args.batch, args.workers, np.random.default_rng(rank))
+    elapsed, task_lat = h.throughput(args.steps, args.warmup, world, dist)
+    value = world * args.workers * args.batch * args.steps / elapsed
 
     result = {
         "metric": BASELINE_METRIC,
@@ -213,7 +263,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -223,54 +273,75 @@ def main():
         "config": {
             "workload": WORKLOADS[args.model],
             "batch_per_task": args.batch,
-            "workers_per_gpu": W,
-            "tasks_per_step_per_gpu": W,
+            "workers_per_gpu": args.workers,
+            "tasks_per_step_per_gpu": args.workers,
+            "precision_mode": {"fp16x3": "split-fp16 MFMA (hi/lo fp16 operands, fp32 accumulate): fp32-grade parity",
+                               "fp16": "fp16 MFMA operands, fp32 accumulate", "fp32": "fp32 MFMA"}[args.precision],
             "graphs": bool(args.graphs),
             "parallelism": f"replicas x{world} (request sharding, no collective)",
         },
-        "p50_task_latency_ms": round(percentile(task_lat_ms, 50), 4),
-        "p95_task_latency_ms": round(percentile(task_lat_ms, 95), 4),
-        "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2e, 50), 4),
-        "e2e_inferences_per_s_serial": round(args.batch / (percentile(e2e, 50) * 1e-3), 2),
-        "model_gflop_per_inference": round(replica.flops(1) / 1e9, 4),
-        "forward_device_ms_profiled": round(fwd_ms, 4),
-        "model_tflops_per_gpu": round(replica.flops(1) * value / world / 1e12, 3),
-        "roofline": {
-            "bound": "mfma",
-            "kernel": dom_name,
-            "launches_per_forward": dom_count,
-            "achieved": round(achieved_tf, 3),
-            "peak": peak,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tf / peak, 5),
-            "traffic": None,
-            "algorithmic_flops_per_launch": dom_flops,
-            "avg_launch_ms": round(dom_ms, 5),
-            "forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5),
-        },
+        "p50_task_latency_ms": round(percentile(task_lat, 50), 4),
+        "p95_task_latency_ms": round(percentile(task_lat, 95), 4),
     }
+    if rank == 0:
+        e2e = h.serial_e2e(args.latency_iters)
+        result["p50_e2e_latency_ms_incl_h2d_d2h"] = round(percentile(e2e, 50), 4)
+        result["e2e_inferences_per_s_serial"] = round(args.batch / (percentile(e2e, 50) * 1e-3), 2)
+        result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
+        result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
+        result["roofline"] = h.dominant_kernel(args.precision)
 
     if rank == 0 and args.cpu_seconds > 0:
         from oracle.cpu_codelet import cpu_inference
 
         cores = torch.get_num_threads()
         n, t_cpu = 0, 0.0
-        x_cpu = host_inputs
-        cpu_inference(model, x_cpu)  # warm-up
+        cpu_inference(model, h.host_inputs)  # warm-up
         while t_cpu < args.cpu_seconds and n < 200:
             ts = time.perf_counter()
-            cpu_inference(model, x_cpu)
+            cpu_inference(model, h.host_inputs)
             t_cpu += time.perf_counter() - ts
             n += 1
         result["cpu_baseline"] = {
-            "value": round(n * args.batch / t_cpu, 3),
-            "unit": "inferences/s",
-            "cores": cores,
-            "kind": "port",
+            "value": round(n * args.batch / t_cpu, 3), "unit": "inferences/s", "cores": cores, "kind": "port",
             "sample": f"{n} forwards of the same {args.model} batch {args.batch} fp32 on host ATen "
                       f"(torch {torch.__version__}, {cores} intra-op threads), {t_cpu:.1f}s",
-            "p50_ms": round(t_cpu / n * 1e3, 3),
-        }
+            "p50_ms": round(t_cpu / n * 1e3, 3)}
+
+    if rank == 0 and world == 1 and args.extras and args.model == "resnet18":
+        extras = {}
+        # plain fp16 operands on the same workload (faster, 1.8e-3 parity on this network)
+        r16 = spi.ModelReplica(model, dev, "fp16", max_batch=args.batch, graphs=True)
+        h16 = Harness(spi, r16, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1))
+        el, lat = h16.throughput(args.steps, args.warmup)
+        extras["resnet18_bs8_fp16_plain"] = {
+            "value": round(args.workers * args.batch * args.steps / el, 2), "unit": "inferences/s",
+            "p50_task_latency_ms": round(percentile(lat, 50), 4), "parity_normalised_max_err": 1.8e-3}
+        # ResNet-18 bs=1 latency (the metric names it)
+        r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
+        h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2))
+        el, lat = h1.throughput(args.steps, args.warmup)
+        e2e1 = h1.serial_e2e(args.latency_iters)
+        extras["resnet18_bs1"] = {"value": round(args.workers * args.steps / el, 2), "unit": "inferences/s",
+                                  "p50_task_latency_ms": round(percentile(lat, 50), 4),
+                                  "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2e1, 50), 4),
+                                  "dtype": args.precision}
+        # the PCIe-inclusive serving path through the mini-runtime (never `value`)
+        extras["resnet18_bs8_runtime_pcie"] = runtime_e2e(spi, replica, "resnet18", args.batch)
+        del r16, h16, r1, h1
+        # BERT-base seq128 bs8 fp16 (BASELINE configs[2])
+        bmodel = zoo.build("bert_base", seed=0)
+        rb = spi.ModelReplica(bmodel, dev, "fp16", max_batch=8, seq_len=seq, graphs=True)
+        hb = Harness(spi, rb, "bert_base", dev, 8, args.workers, np.random.default_rng(3))
+        el, lat = hb.throughput(max(20, args.steps // 4), 5)
+        e2eb = hb.serial_e2e(10)
+        extras["bert_base_seq128_bs8_fp16"] = {
+            "value": round(args.workers * 8 * max(20, args.steps // 4) / el, 2), "unit": "sequences/s",
+            "p50_task_latency_ms": round(percentile(lat, 50), 4),
+            "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2eb, 50), 4),
+            "gflop_per_seq": round(rb.flops(1) / 1e9, 3), "roofline": hb.dominant_kernel("fp16")}
+        result["extras"] = extras
+
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

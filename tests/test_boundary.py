@@ -40,14 +40,17 @@ def test_library_exports_every_header_symbol(spi):
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     missing = sorted(names - exported)
     assert not missing, f"declared but not exported: {missing}"
+    import importlib
+    importlib.import_module("starpu-inference-server_amd.runtime")  # binds include/spi_runtime.h
     for n in names:  # and every one is bound in ctypes
-        assert n in spi._native._PROTOS, n
+        assert n in spi._native._PROTOS or getattr(spi.lib, n).argtypes is not None, n
 
 
 PROBE = r"""
 #include <stdio.h>
 #include <stddef.h>
 #include "spi_codelet.h"
+#include "spi_runtime.h"
 #define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 #define S(T) printf(#T " %zu\n", sizeof(T));
 int main(void) {
@@ -59,6 +62,9 @@ int main(void) {
   F(spi_codelet_args, output_types) F(spi_codelet_args, model_cpu) F(spi_codelet_args, cpu_forward)
   F(spi_codelet_args, device_ids) F(spi_codelet_args, models_gpu) F(spi_codelet_args, codelet_start_ns)
   F(spi_codelet_args, executed_on) F(spi_codelet_args, status) F(spi_codelet_args, error)
+  S(spi_runtime_config) F(spi_runtime_config, models) F(spi_runtime_config, workers_per_device)
+  F(spi_runtime_config, input_dims) F(spi_runtime_config, num_outputs) F(spi_runtime_config, output_elems)
+  S(spi_job_timing) F(spi_job_timing, complete_ns) F(spi_job_timing, worker_id)
   return 0;
 }
 """
@@ -71,8 +77,11 @@ def test_ctypes_layouts_match_the_c_header(spi, tmp_path):
     subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                              check=True).stdout.splitlines())
+    import importlib
+    rt = importlib.import_module("starpu-inference-server_amd.runtime")
     N = spi._native
-    types = {"spi_vector_interface": N.VectorInterface, "spi_variable_interface": N.VariableInterface,
+    types = {"spi_runtime_config": rt.RuntimeConfig, "spi_job_timing": rt.JobTiming,
+             "spi_vector_interface": N.VectorInterface, "spi_variable_interface": N.VariableInterface,
              "spi_tensor_view": N.TensorView, "spi_named_tensor": N.NamedTensor, "spi_model_config": N.ModelConfig,
              "spi_codelet_args": N.CodeletArgs}
     for key, val in got.items():
@@ -271,3 +280,19 @@ def test_no_fallback_when_library_missing(tmp_path):
     code = "import importlib, sys; sys.path.insert(0, %r); importlib.import_module('starpu-inference-server_amd')"
     r = subprocess.run([sys.executable, "-c", code % str(tmp_path)], capture_output=True, text=True)
     assert r.returncode != 0 and "libspi_hip.so is missing" in r.stderr
+
+
+def test_runtime_rejects_invalid_config_without_touching_a_device(spi):
+    import importlib
+    rt = importlib.import_module("starpu-inference-server_amd.runtime")
+    cfg = rt.RuntimeConfig()  # zero devices
+    err = C.create_string_buffer(128)
+    assert not spi.lib.spi_runtime_create(C.byref(cfg), err, 128)
+    assert b"invalid runtime configuration" in err.value
+    cfg.num_devices, cfg.max_batch, cfg.num_inputs, cfg.num_outputs = 1, 8, 1, 1
+    cfg.input_types[0], cfg.input_ndims[0] = 6, 1
+    cfg.input_dims[0][0] = 4
+    cfg.output_types[0], cfg.output_elems[0] = 6, 4
+    assert not spi.lib.spi_runtime_create(C.byref(cfg), err, 128)  # no replica for the device
+    assert b"missing replica" in err.value
+    assert spi.lib.spi_runtime_submit(None, 0, 1, None, None, rt.DONE_FN(), None) == spi._native.SPI_ERR_INVALID_ARGUMENT

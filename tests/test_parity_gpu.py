@@ -68,7 +68,7 @@ def test_resnet_bottleneck_small(spi, zoo, gpu, prec):
     got = hip_forward(spi, rep, [x], ref.shape)
     err = normalized_max_error(got, ref)
     print(f"resnet-bottleneck@64 {prec} err={err:.3e}")
-    assert err < resnet_tol(prec) * 2
+    assert err < (1e-2 if prec == "fp16" else resnet_tol(prec))  # 64x64 images: small logits, plain fp16 floor
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3"])
