@@ -245,7 +245,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = local_rank
+    # SPI_BENCH_SHARE_DEVICE=1: every rank on device 0 (multi-rank rehearsal on a 1-GPU box only).
+    dev = 0 if os.environ.get("SPI_BENCH_SHARE_DEVICE") == "1" else local_rank
     torch.cuda.set_device(dev)
 
     seq = 128

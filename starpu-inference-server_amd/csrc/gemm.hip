@@ -40,7 +40,6 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int ROWB = 128;  // bytes per image row per k-step
 
 struct KArgs {
   GemmDesc d;
@@ -55,23 +54,25 @@ struct KArgs {
 
 template <int MODE>
 struct Traits;
+// RB: bytes of each A / W image row per k-step; ESTEP: k-values per step;
+// EPC: A elements per 16-byte chunk.
 template <>
 struct Traits<(int)Prec::F16> {
   using A = _Float16;
   using Out = _Float16;
-  static constexpr int ESTEP = 64, EPC = 8;  // k per step, A elements per 16-B chunk
+  static constexpr int RB = 128, ESTEP = 64, EPC = 8;
 };
 template <>
 struct Traits<(int)Prec::F32> {
   using A = float;
   using Out = float;
-  static constexpr int ESTEP = 32, EPC = 4;
+  static constexpr int RB = 128, ESTEP = 32, EPC = 4;
 };
 template <>
-struct Traits<(int)Prec::F16X3> {
+struct Traits<(int)Prec::F16X3> {  // A: 32 fp32; W: [32 hi | 32 lo] (RB = 256 measured slower: VGPRs, LDS)
   using A = float;
   using Out = float;
-  static constexpr int ESTEP = 32, EPC = 4;
+  static constexpr int RB = 128, ESTEP = 32, EPC = 4;
 };
 
 __device__ __forceinline__ float apply_act(float v, Act act) {
@@ -125,17 +126,21 @@ __device__ __forceinline__ void dma_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+template <int RB>
 __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
-  return *reinterpret_cast<const u32x4*>(img + row * ROWB + ((c ^ (row & 7)) << 4));
+  constexpr int CPR = RB / 16;  // 16-byte chunks per image row
+  return *reinterpret_cast<const u32x4*>(img + row * RB + ((c ^ (row & (CPR - 1))) << 4));
 }
 
 template <int MODE, int BM, int BN, int STAGES, bool CONV>
 __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   using TR = Traits<MODE>;
   using AT = typename TR::A;
-  constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC;
-  constexpr int IMG = (BM + BN) * ROWB;  // bytes per stage
-  constexpr int AQ = BM / 32, BQ = BN / 32;  // DMA instructions per wave per step
+  constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
+  constexpr int CPR = RB / 16;             // chunks per image row
+  constexpr int RPI = 64 / CPR;            // image rows per 1-KiB DMA instruction
+  constexpr int IMG = (BM + BN) * RB;      // bytes per stage
+  constexpr int AQ = BM / RPI / 4, BQ = BN / RPI / 4;  // DMA instructions per wave per step
   constexpr int QPS = AQ + BQ;
   __shared__ __attribute__((aligned(16))) char lds[STAGES * IMG + 16];
   int* s_flag = reinterpret_cast<int*>(lds + STAGES * IMG);
@@ -159,15 +164,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   const char* __restrict__ Wb = static_cast<const char*>(a.p.W);
 
   // Per-lane source bookkeeping (fixed across k-steps).
-  const int slot = lane & 7;
+  const int slot = lane & (CPR - 1);
   int a_koff[AQ], a_ih0[AQ], a_iw0[AQ];
   bool a_ok[AQ];
   const AT* a_base[AQ];
   const AT* a_pix[AQ];  // conv: image pointer at (ih0, iw0), may point before the image
 #pragma unroll
   for (int q = 0; q < AQ; ++q) {
-    const int r = (wave * AQ + q) * 8 + (lane >> 3);
-    a_koff[q] = (slot ^ (r & 7)) * EPC;
+    const int r = (wave * AQ + q) * RPI + lane / CPR;
+    a_koff[q] = (slot ^ (r & (CPR - 1))) * EPC;
     const int m = m0 + r;
     a_ok[q] = m < d.M;
     const int mm = a_ok[q] ? m : 0;
@@ -190,8 +195,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   const char* b_src[BQ];
 #pragma unroll
   for (int q = 0; q < BQ; ++q) {
-    const int r = (wave * BQ + q) * 8 + (lane >> 3);
-    const int c = slot ^ (r & 7);
+    const int r = (wave * BQ + q) * RPI + lane / CPR;
+    const int c = slot ^ (r & (CPR - 1));
     // W rows are Kpad elements (F16/F32) or 2*Kpad fp16 (F16X3, 64-element blocks of hi|lo).
     const size_t row_bytes = (MODE == (int)Prec::F16) ? (size_t)d.Kpad * 2 : (size_t)d.Kpad * 4;
     b_src[q] = Wb + (size_t)(n0 + r) * row_bytes + c * 16;
@@ -240,12 +245,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
-    // k-step byte offset inside a W row: 128 B per step in every mode.
-    const size_t kb = (size_t)(k0 / ESTEP) * ROWB;
+    // k-step byte offset inside a W row: RB bytes per step.
+    const size_t kb = (size_t)(k0 / ESTEP) * RB;
 #pragma unroll
     for (int q = 0; q < BQ; ++q)
       __builtin_amdgcn_global_load_lds((const void*)(b_src[q] + kb),
-                                       (lds_ptr_t)(dst + BM * ROWB + (wave * BQ + q) * 1024), 16, 0, 0);
+                                       (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
   };
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -303,17 +308,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
     }
     if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
     const char* As = lds + (t % STAGES) * IMG;
-    const char* Bs = As + BM * ROWB;
+    const char* Bs = As + BM * RB;
     if constexpr (MODE == (int)Prec::F16) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         half8 af[TI], bf[TJ];
 #pragma unroll
         for (int i = 0; i < TI; ++i)
-          af[i] = __builtin_bit_cast(half8, rd_chunk(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
+          af[i] = __builtin_bit_cast(half8, rd_chunk<RB>(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          bf[j] = __builtin_bit_cast(half8, rd_chunk(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
+          bf[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -321,39 +326,42 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
       }
     } else if constexpr (MODE == (int)Prec::F16X3) {
-      half8 ah[TI], al[TI], bh[TJ], bl[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int row = wm * WTM + i * 16 + fr;
-        split8(rd_chunk(As, row, 2 * fq), rd_chunk(As, row, 2 * fq + 1), ah[i], al[i]);
-      }
+      for (int kk = 0; kk < ESTEP / 32; ++kk) {
+        half8 ah[TI], al[TI], bh[TJ], bl[TJ];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int row = wn * WTN + j * 16 + fr;
-        bh[j] = __builtin_bit_cast(half8, rd_chunk(Bs, row, fq));
-        bl[j] = __builtin_bit_cast(half8, rd_chunk(Bs, row, 4 + fq));
-      }
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i) {
+          const int row = wm * WTM + i * 16 + fr;
+          split8(rd_chunk<RB>(As, row, kk * 8 + 2 * fq), rd_chunk<RB>(As, row, kk * 8 + 2 * fq + 1), ah[i], al[i]);
+        }
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          const int row = wn * WTN + j * 16 + fr;
+          bh[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, kk * 8 + fq));
+          bl[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, kk * 8 + 4 + fq));
         }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      }
     } else {
       floatx4 a0[TI], a1[TI], b0[TJ], b1[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wm * WTM + i * 16 + fr;
-        a0[i] = __builtin_bit_cast(floatx4, rd_chunk(As, row, 2 * fq));
-        a1[i] = __builtin_bit_cast(floatx4, rd_chunk(As, row, 2 * fq + 1));
+        a0[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(As, row, 2 * fq));
+        a1[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(As, row, 2 * fq + 1));
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int row = wn * WTN + j * 16 + fr;
-        b0[j] = __builtin_bit_cast(floatx4, rd_chunk(Bs, row, 2 * fq));
-        b1[j] = __builtin_bit_cast(floatx4, rd_chunk(Bs, row, 2 * fq + 1));
+        b0[j] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Bs, row, 2 * fq));
+        b1[j] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Bs, row, 2 * fq + 1));
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -458,7 +466,10 @@ struct Plan {
   int bm, bn, stages, splits, k_per_split;
 };
 
-int estep_of(Prec prec) { return prec == Prec::F16 ? 64 : 32; }
+int estep_of(Prec prec) {
+  return prec == Prec::F16 ? Traits<(int)Prec::F16>::ESTEP
+                           : prec == Prec::F32 ? Traits<(int)Prec::F32>::ESTEP : Traits<(int)Prec::F16X3>::ESTEP;
+}
 
 // Tuning hook: SPI_GEMM_PLAN="bm,bn,stages,splits" forces the plan (micro-benchmarks only).
 bool plan_override(Plan* pl) {

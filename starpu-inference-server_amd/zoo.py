@@ -113,10 +113,23 @@ class ResNet(nn.Module):
 
 def _randomize_bn_and_calibrate(model: nn.Module, image: int, seed: int, calib_batch: int = 4) -> None:
     g = torch.Generator().manual_seed(seed + 1)
+    # The last BN of each residual branch gets a small gamma, as in trained
+    # ResNets (torchvision's zero_init_residual idea, kept non-zero): with unit
+    # gammas a random 50-block ResNet-152 amplifies fp32 rounding to ~5e-4
+    # (fp32 vs fp64 on CPU), which would make any parity check meaningless.
+    last_bn = set()
+    for blk in model.modules():
+        if isinstance(blk, Bottleneck):
+            last_bn.add(id(blk.bn3))
+        elif isinstance(blk, BasicBlock):
+            last_bn.add(id(blk.bn2))
     for m in model.modules():
         if isinstance(m, nn.BatchNorm2d):
             with torch.no_grad():
-                m.weight.copy_(0.75 + 0.5 * torch.rand(m.num_features, generator=g))
+                if id(m) in last_bn:
+                    m.weight.copy_(0.1 + 0.3 * torch.rand(m.num_features, generator=g))
+                else:
+                    m.weight.copy_(0.75 + 0.5 * torch.rand(m.num_features, generator=g))
                 m.bias.copy_(0.2 * torch.rand(m.num_features, generator=g) - 0.1)
             m.momentum = None  # cumulative average: one pass = that batch's statistics
             m.reset_running_stats()
