@@ -41,6 +41,21 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 
+// Diagnostic build only (-DSPI_GEMM_STAMPS): per-block s_memtime phase totals.
+#ifdef SPI_GEMM_STAMPS
+__device__ unsigned long long g_gemm_stamps[65536 * 8];
+#define SPI_STAMP(v)                                                                         \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+  } while (0)
+#else
+#define SPI_STAMP(v) \
+  do {               \
+  } while (0)
+#endif
+
 struct KArgs {
   GemmDesc d;
   GemmPtrs p;
@@ -289,7 +304,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
         rpre[i][j][r] = (pre && a.p.res && m < d.M && n < d.N) ? load_res<MODE>(a, m, n) : 0.f;
       }
 
+  unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
+  SPI_STAMP(st_t0);
   for (int t = 0; t < nsteps; ++t) {
+    SPI_STAMP(st_a);
     // Step t has landed once at most (issued steps after t) DMA groups remain.
     if constexpr (STAGES == 4) {
       if (t + 2 < nsteps)
@@ -306,7 +324,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
     } else {
       dma_wait_barrier<0>();
     }
+    SPI_STAMP(st_b);
     if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    SPI_STAMP(st_c);
     const char* As = lds + (t % STAGES) * IMG;
     const char* Bs = As + BM * RB;
     if constexpr (MODE == (int)Prec::F16) {
@@ -378,8 +398,30 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][s], b1[j][s], acc[i][j], 0, 0, 0);
     }
+#ifdef SPI_GEMM_STAMPS
+    // MFMA results are consumed only at the end; force completion so the compute phase is timed.
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) asm volatile("" ::"v"(acc[i][j]));
+#endif
+    SPI_STAMP(st_d);
+    st_wait += st_b - st_a;
+    st_issue += st_c - st_b;
+    st_comp += st_d - st_c;
   }
 
+  SPI_STAMP(st_d);
+#ifdef SPI_GEMM_STAMPS
+  if (tid == 0) {
+    unsigned long long* g = g_gemm_stamps + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) & 65535) * 8;
+    g[0] = st_d - st_t0;
+    g[1] = st_wait;
+    g[2] = st_issue;
+    g[3] = st_comp;
+    g[4] = (unsigned long long)nsteps;
+  }
+#endif
   if (gridDim.y == 1) {
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -575,6 +617,12 @@ size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
 }
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }
+
+#ifdef SPI_GEMM_STAMPS
+extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   switch (prec) {
