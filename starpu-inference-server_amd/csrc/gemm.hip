@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace spi {
 namespace {
@@ -278,21 +279,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nsteps) issue(s, s);
-
-  // Epilogue operands fetched now so their latency hides under the K loop
-  // (single-slice tiles only; the split-K reducer reads them itself).
-  // Only small tiles (16 accumulators per lane) can spare the registers.
+  // Epilogue operands fetched before the first DMAs so their latency hides
+  // under the K loop and the counted vmcnt waits never stall on them (single-
+  // slice tiles only; the split-K reducer reads them itself).  Only small
+  // tiles (16 accumulators per lane) can spare the registers.  The residual is
+  // held in its storage type (Out) and converted in the epilogue: converting
+  // here would force a vmcnt(0) per element.  F16 with an fp32 residual takes
+  // the per-element epilogue.  Out-of-tile lanes read element 0.
+  using Out = typename Traits<MODE>::Out;
   constexpr bool kPrefetch = TI * TJ <= 4;
-  const bool pre = kPrefetch && gridDim.y == 1;
-  float rpre[TI][TJ][4], bpre[TJ];
+  const bool pre = kPrefetch && gridDim.y == 1 && (sizeof(Out) == 4 || !d.res_f32);
+  float bpre[TJ];
+  Out rpre[TI][TJ][4];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int n = n0 + wn * WTN + j * 16 + fr;
-    bpre[j] = (pre && a.p.bias && n < d.N) ? a.p.bias[n] : 0.f;
+    bpre[j] = (pre && a.p.bias ? a.p.bias : reinterpret_cast<const float*>(zeros))[pre && a.p.bias && n < d.N ? n : 0];
   }
+  // No branch around the loads (LLVM would sink the conversion into it):
+  // tiles without a residual read the zero line.
+  const bool use_res = pre && a.p.res;
+  const Out* R = use_res ? static_cast<const Out*>(a.p.res) : reinterpret_cast<const Out*>(zeros);
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -301,10 +308,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
         const int n = n0 + wn * WTN + j * 16 + fr;
-        rpre[i][j][r] = (pre && a.p.res && m < d.M && n < d.N) ? load_res<MODE>(a, m, n) : 0.f;
+        rpre[i][j][r] = R[(use_res && m < d.M && n < d.N) ? (size_t)m * d.ldr + n : 0];
       }
 
-  unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nsteps) issue(s, s);
+
+  [[maybe_unused]] unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
   SPI_STAMP(st_t0);
   for (int t = 0; t < nsteps; ++t) {
     SPI_STAMP(st_a);
@@ -325,50 +336,62 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
       dma_wait_barrier<0>();
     }
     SPI_STAMP(st_b);
-    if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
-    SPI_STAMP(st_c);
+    // All of this step's fragment reads go out first, then the next step's
+    // DMAs (their issue cost overlaps the LDS latency), then the MFMAs.
     const char* As = lds + (t % STAGES) * IMG;
     const char* Bs = As + BM * RB;
+    auto issue_next = [&] {
+      if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    };
     if constexpr (MODE == (int)Prec::F16) {
+      half8 af[2][TI], bf[2][TJ];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        half8 af[TI], bf[TJ];
 #pragma unroll
         for (int i = 0; i < TI; ++i)
-          af[i] = __builtin_bit_cast(half8, rd_chunk<RB>(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
+          af[kk][i] = __builtin_bit_cast(half8, rd_chunk<RB>(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          bf[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
+          bf[kk][j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
+      }
+      issue_next();
+      SPI_STAMP(st_c);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
     } else if constexpr (MODE == (int)Prec::F16X3) {
+      static_assert(ESTEP == 32, "one 32-k block per step");
+      u32x4 ar0[TI], ar1[TI];
+      half8 bh[TJ], bl[TJ];
 #pragma unroll
-      for (int kk = 0; kk < ESTEP / 32; ++kk) {
-        half8 ah[TI], al[TI], bh[TJ], bl[TJ];
+      for (int i = 0; i < TI; ++i) {
+        const int row = wm * WTM + i * 16 + fr;
+        ar0[i] = rd_chunk<RB>(As, row, 2 * fq);
+        ar1[i] = rd_chunk<RB>(As, row, 2 * fq + 1);
+      }
 #pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          const int row = wm * WTM + i * 16 + fr;
-          split8(rd_chunk<RB>(As, row, kk * 8 + 2 * fq), rd_chunk<RB>(As, row, kk * 8 + 2 * fq + 1), ah[i], al[i]);
-        }
+      for (int j = 0; j < TJ; ++j) {
+        const int row = wn * WTN + j * 16 + fr;
+        bh[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, fq));
+        bl[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, 4 + fq));
+      }
+      issue_next();
+      SPI_STAMP(st_c);
+      half8 ah[TI], al[TI];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) split8(ar0[i], ar1[i], ah[i], al[i]);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const int row = wn * WTN + j * 16 + fr;
-          bh[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, kk * 8 + fq));
-          bl[j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, row, kk * 8 + 4 + fq));
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-          }
-      }
     } else {
       floatx4 a0[TI], a1[TI], b0[TJ], b1[TJ];
 #pragma unroll
@@ -383,6 +406,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
         b0[j] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Bs, row, 2 * fq));
         b1[j] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Bs, row, 2 * fq + 1));
       }
+      issue_next();
+      SPI_STAMP(st_c);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -432,8 +457,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
           const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
           const int n = n0 + wn * WTN + j * 16 + fr;
           if (m < d.M && n < d.N) {
-            if constexpr (kPrefetch)
-              store_out<MODE>(a, m, n, apply_act(acc[i][j][r] + bpre[j] + rpre[i][j][r], d.act));
+            if (pre)
+              store_out<MODE>(a, m, n, apply_act(acc[i][j][r] + bpre[j] + static_cast<float>(rpre[i][j][r]), d.act));
             else
               epilogue_store<MODE>(a, m, n, acc[i][j][r]);
           }
@@ -513,9 +538,10 @@ int estep_of(Prec prec) {
                            : prec == Prec::F32 ? Traits<(int)Prec::F32>::ESTEP : Traits<(int)Prec::F16X3>::ESTEP;
 }
 
-// Tuning hook: SPI_GEMM_PLAN="bm,bn,stages,splits" forces the plan (micro-benchmarks only).
+// Tuning hook: SPI_GEMM_PLAN="bm,bn,stages,splits" forces the plan (micro-benchmarks
+// only; read on every call so a sweep can change it in-process).
 bool plan_override(Plan* pl) {
-  static const char* env = std::getenv("SPI_GEMM_PLAN");
+  const char* env = std::getenv("SPI_GEMM_PLAN");
   if (!env || !*env) return false;
   int bm = 0, bn = 0, st = 0, sp = 0;
   if (std::sscanf(env, "%d,%d,%d,%d", &bm, &bn, &st, &sp) != 4) return false;
@@ -538,25 +564,32 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
     forced.splits = (ksteps + kt_per - 1) / kt_per;
     return forced;
   }
-  static const int cfg[3][2] = {{128, 128}, {128, 64}, {64, 64}};
-  Plan pl{64, 64, 2, 1, d.Kpad};
-  for (auto& c : cfg) {
-    if (c[1] == 128 && d.N <= 64) continue;
-    const int tiles = ((d.M + c[0] - 1) / c[0]) * ((d.N + c[1] - 1) / c[1]);
-    if (tiles >= kTarget) {
-      pl.bm = c[0];
-      pl.bn = c[1];
-      pl.stages = (c[0] == 128 && c[1] == 128) ? 2 : (c[0] == 64 && ksteps < 16 ? 2 : 3);
-      return pl;
-    }
+  // Measured on ResNet-18 / BERT-base / ViT-L layer shapes (tools/gemm_bench.py
+  // --plans): 64x64 tiles win unless the grid is very large; what small-M
+  // layers need is more workgroups per CU, which split-K supplies.
+  const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
+  if (const char* pol = std::getenv("SPI_GEMM_POLICY"); pol && std::strncmp(pol, "tput:", 5) == 0) {
+    // Experiment: largest tile with >= T tiles, no split-K unless 64x64 falls short.
+    const int T = std::max(1, std::atoi(pol + 5));
+    if (d.N > 64 && tiles_of(128, 128) >= T) return Plan{128, 128, 2, 1, d.Kpad};
+    if (tiles_of(128, 64) >= T) return Plan{128, 64, ksteps >= 16 ? 3 : 2, 1, d.Kpad};
+    const int t64 = tiles_of(64, 64);
+    const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
+    const int kt = (ksteps + sp - 1) / sp;
+    return Plan{64, 64, kt >= 16 ? 3 : 2, (ksteps + kt - 1) / kt, kt * ES};
   }
-  const int tiles = ((d.M + 63) / 64) * ((d.N + 63) / 64);
+  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return Plan{128, 128, 2, 1, d.Kpad};
+  if (prec == Prec::F16 && tiles_of(128, 64) >= 384 && ksteps >= 32) return Plan{128, 64, 3, 1, d.Kpad};
+  const int tiles = tiles_of(64, 64);
   int splits = 1;
-  if (tiles < kTarget / 2 && ksteps >= 6) splits = std::max(1, std::min(ksteps / 3, (2 * kTarget + tiles - 1) / tiles));
+  if (tiles < kTarget) {
+    const int want = (prec == Prec::F16 ? 384 : 512) / tiles;  // workgroups per launch
+    splits = std::max(1, std::min(want, ksteps / 6));            // >= 6 k-steps per slice
+  }
   const int kt_per = (ksteps + splits - 1) / splits;
+  Plan pl{64, 64, kt_per >= 16 ? 3 : 2, 1, 0};  // a deeper ring pays only on long K loops
   pl.k_per_split = kt_per * ES;
   pl.splits = (ksteps + kt_per - 1) / kt_per;
-  pl.stages = kt_per >= 16 ? 3 : 2;  // a deeper ring pays only on long K loops
   return pl;
 }
 

@@ -15,7 +15,7 @@ namespace {
 
 constexpr size_t kZeroBytes = 256;
 constexpr size_t kTickets = 16384;
-constexpr size_t kSlabFloats = (size_t)640 * 64 * 64;
+constexpr size_t kSlabFloats = (size_t)8 << 20;  // 32 MiB of split-K slabs
 
 bool prec_of(int32_t p, spi::Prec* out) {
   if (p == 0) *out = spi::Prec::F32;

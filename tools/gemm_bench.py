@@ -17,8 +17,9 @@ ops = importlib.import_module("starpu-inference-server_amd.ops")
 
 # (name, B, H, Cin, Cout, k, stride)  ResNet-18 bs8 layer shapes (+ stem with Cin padded to 8)
 CONVS = [("stem7x7", 8, 224, 8, 64, 7, 2), ("l1_3x3", 8, 56, 64, 64, 3, 1), ("l2_3x3s2", 8, 56, 64, 128, 3, 2),
-         ("l2_3x3", 8, 28, 128, 128, 3, 1), ("l3_3x3", 8, 14, 256, 256, 3, 1), ("l4_3x3", 8, 7, 512, 512, 3, 1),
-         ("l4_ds1x1", 8, 14, 256, 512, 1, 2)]
+         ("l2_ds1x1", 8, 56, 64, 128, 1, 2), ("l2_3x3", 8, 28, 128, 128, 3, 1), ("l3_3x3s2", 8, 28, 128, 256, 3, 2),
+         ("l3_ds1x1", 8, 28, 128, 256, 1, 2), ("l3_3x3", 8, 14, 256, 256, 3, 1), ("l4_3x3s2", 8, 14, 256, 512, 3, 2),
+         ("l4_ds1x1", 8, 14, 256, 512, 1, 2), ("l4_3x3", 8, 7, 512, 512, 3, 1)]
 # (name, M, N, K)  BERT-base bs8 S128 / ViT-L bs16
 GEMMS = [("bert_qkv", 1024, 2304, 768), ("bert_out", 1024, 768, 768), ("bert_ff1", 1024, 3072, 768),
          ("bert_ff2", 1024, 768, 3072), ("vit_qkv", 3152, 3072, 1024), ("vit_ff1", 3152, 4096, 1024),
@@ -49,7 +50,20 @@ def main():
     ap.add_argument("--prec", default="fp16")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
+    ap.add_argument("--plans", default="", help="';'-separated SPI_GEMM_PLAN values to sweep ('' = the chooser)")
     a = ap.parse_args()
+    plans = a.plans.split(";") if a.plans else [""]
+
+    def sweep(fn, label, fl):
+        for plan in plans:
+            os.environ["SPI_GEMM_PLAN"] = plan
+            try:
+                ms = timeit(fn, a.reps)
+            except ops.OpError as e:
+                print(f"{label}  skipped: {e}  [{plan}]", flush=True)
+                continue
+            print(f"{label}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s  [{plan or 'auto'}]", flush=True)
+        os.environ["SPI_GEMM_PLAN"] = ""
     dt = ops.act_dtype(a.prec)
     ws = ops.workspace()
     rng = np.random.default_rng(0)
@@ -62,9 +76,9 @@ def main():
         pad = k // 2
         oh = (H + 2 * pad - k) // st + 1
         out = torch.empty(B, oh, oh, cout, device="cuda", dtype=dt)
-        ms = timeit(lambda: ops.conv2d(a.prec, x, wp, cout, k, k, st, pad, ws=ws, out=out), a.reps)
         fl = 2.0 * B * oh * oh * cout * k * k * cin
-        print(f"conv {name:10s} M={B*oh*oh:6d} N={cout:4d} K={k*k*cin:5d}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s")
+        sweep(lambda: ops.conv2d(a.prec, x, wp, cout, k, k, st, pad, ws=ws, out=out),
+              f"conv {name:10s} M={B*oh*oh:6d} N={cout:4d} K={k*k*cin:5d}", fl)
     for name, M, N_, K in GEMMS:
         if a.only and a.only not in name:
             continue
@@ -72,9 +86,8 @@ def main():
         w = rng.standard_normal((N_, K)).astype(np.float32) * 0.05
         wp = ops.pack_weight(a.prec, w)
         out = torch.empty(M, N_, device="cuda", dtype=torch.float32)
-        ms = timeit(lambda: ops.gemm(a.prec, A, wp, N_, out=out, ws=ws), a.reps)
         fl = 2.0 * M * N_ * K
-        print(f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s")
+        sweep(lambda: ops.gemm(a.prec, A, wp, N_, out=out, ws=ws), f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d}", fl)
 
 
 if __name__ == "__main__":
