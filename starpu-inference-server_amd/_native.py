@@ -17,7 +17,8 @@ import os
 import torch  # noqa: F401  (pins the process-wide HIP runtime, see docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspi_hip.so")
+# SPI_HIP_LIB: another build of the same library (A/B runs, tools/build_variant.sh).
+LIB_PATH = os.environ.get("SPI_HIP_LIB") or os.path.join(_HERE, "libspi_hip.so")
 
 SPI_ABI_VERSION = 1
 SPI_MAX_INPUTS = 16

@@ -73,6 +73,94 @@ __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int B
   }
 }
 
+// F16X3 split activations: per pixel, C/32 blocks of [32 hi | 32 lo] fp16.
+// Channel group g (8 channels) has its hi vector at fp16 offset split_goff(g)
+// and its lo vector 32 further on.
+__device__ __forceinline__ int split_goff(int g) { return (g >> 2) * 64 + (g & 3) * 8; }
+
+__device__ __forceinline__ void split_load8(const _Float16* p, float v[8]) {
+  const uint4 h = *reinterpret_cast<const uint4*>(p);
+  const uint4 l = *reinterpret_cast<const uint4*>(p + 32);
+  const _Float16* hh = reinterpret_cast<const _Float16*>(&h);
+  const _Float16* ll = reinterpret_cast<const _Float16*>(&l);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = static_cast<float>(hh[q]) + static_cast<float>(ll[q]);
+}
+
+__device__ __forceinline__ void split_store8(_Float16* p, const float v[8]) {
+  _Float16 h[8], l[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    h[q] = static_cast<_Float16>(v[q]);
+    l[q] = static_cast<_Float16>(v[q] - static_cast<float>(h[q]));
+  }
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(h);
+  *reinterpret_cast<uint4*>(p + 32) = *reinterpret_cast<const uint4*>(l);
+}
+
+// Max pool split -> split; one thread per (output pixel, 8-channel group).
+__global__ void maxpool_split_kernel(const _Float16* __restrict__ x, _Float16* __restrict__ y, int B, int H,
+                                     int W, int C, int OH, int OW, int k, int stride, int pad) {
+  const int G = C / 8;
+  const size_t n = (size_t)B * OH * OW * G;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const size_t pix = i / G;
+    const int ow = (int)(pix % OW);
+    const size_t r = pix / OW;
+    const int oh = (int)(r % OH);
+    const int b = (int)(r / OH);
+    float m[8], v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * stride - pad + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * stride - pad + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        split_load8(x + (((size_t)b * H + ih) * W + iw) * C * 2 + split_goff(g), v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], v[q]);
+      }
+    }
+    split_store8(y + pix * C * 2 + split_goff(g), m);
+  }
+}
+
+// Average pool split -> fp32 [B, C]; one block per image, thread (p, g) sums
+// pixels p, p+P, ... of channel group g, the P partial sums meet in LDS.
+__global__ __launch_bounds__(256) void avgpool_split_kernel(const _Float16* __restrict__ x, float* __restrict__ y,
+                                                            int HW, int C) {
+  __shared__ float part[256 * 8];
+  const int b = blockIdx.x, G = C / 8;
+  const _Float16* img = x + (size_t)b * HW * C * 2;
+  for (int g0 = 0; g0 < G; g0 += 256) {
+    const int Gc = min(256, G - g0);
+    const int P = 256 / Gc;
+    const int p = threadIdx.x / Gc, g = g0 + threadIdx.x % Gc;
+    float s[8] = {}, v[8];
+    if (p < P)
+      for (int px = p; px < HW; px += P) {
+        split_load8(img + (size_t)px * C * 2 + split_goff(g), v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += v[q];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part[threadIdx.x * 8 + q] = s[q];
+    __syncthreads();
+    if (threadIdx.x < Gc) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float t = 0.f;
+        for (int pp = 0; pp < P; ++pp) t += part[(pp * Gc + threadIdx.x) * 8 + q];
+        y[(size_t)b * C + (size_t)(g0 + threadIdx.x) * 8 + q] = t / (float)HW;
+      }
+    }
+  }
+}
+
 // Global average pool: one block per image; thread (g, c) sums pixels g, g+G, ...
 // of its 16-byte channel vector c, then the G partial sums meet in LDS.
 template <typename T>
@@ -279,6 +367,17 @@ void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH, in
   else
     hipLaunchKernelGGL((maxpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
                        (const float*)x, (float*)y, B, H, W, C, OH, OW, k, stride, pad);
+}
+
+void maxpool_nhwc_split(const void* x, void* y, int B, int H, int W, int C, int OH, int OW, int k, int stride,
+                        int pad, hipStream_t s) {
+  const size_t n = (size_t)B * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_split_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const _Float16*)x, (_Float16*)y, B,
+                     H, W, C, OH, OW, k, stride, pad);
+}
+
+void avgpool_nhwc_split(const void* x, float* y, int B, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B), dim3(256), 0, s, (const _Float16*)x, y, HW, C);
 }
 
 void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s) {

@@ -32,6 +32,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
+#include <stdexcept>
 
 namespace spi {
 namespace {
@@ -90,6 +92,22 @@ struct Traits<(int)Prec::F16X3> {  // A: 32 fp32; W: [32 hi | 32 lo] (RB = 256 m
   using Out = float;
   static constexpr int RB = 128, ESTEP = 32, EPC = 4;
 };
+// Kernel-internal mode: F16X3 whose A (and residual) are activations already
+// stored split, [32 hi fp16 | 32 lo fp16] per 32 channels (GemmDesc::a_split).
+// Byte-for-byte the same addressing as fp32 A (a 32-k block is 128 bytes either
+// way), so only the fragment reads differ: A is read exactly like W.
+constexpr int kF16X3S = 3;
+template <>
+struct Traits<kF16X3S> : Traits<(int)Prec::F16X3> {};
+
+template <int MODE>
+constexpr bool kSplitMode = MODE == (int)Prec::F16X3 || MODE == kF16X3S;
+
+// Split layout index (in fp16 units) of logical element (m, n) of a row-major
+// [rows][ld] tensor: hi at the returned index, lo 32 further on.
+__device__ __forceinline__ size_t split_idx(int m, int n, int ld) {
+  return (size_t)m * ld * 2 + (size_t)(n >> 5) * 64 + (n & 31);
+}
 
 __device__ __forceinline__ float apply_act(float v, Act act) {
   if (act == Act::Relu) return v > 0.f ? v : 0.f;
@@ -100,25 +118,14 @@ __device__ __forceinline__ float apply_act(float v, Act act) {
 template <int MODE>
 __device__ __forceinline__ float load_res(const KArgs& a, int m, int n) {
   using Out = typename Traits<MODE>::Out;
+  if constexpr (MODE == kF16X3S) {  // split residual: hi + lo
+    const _Float16* R = static_cast<const _Float16*>(a.p.res);
+    const size_t i = split_idx(m, n, a.d.ldr);
+    return static_cast<float>(R[i]) + static_cast<float>(R[i + 32]);
+  }
   const size_t idx = (size_t)m * a.d.ldr + n;
   return a.d.res_f32 ? static_cast<const float*>(a.p.res)[idx]
                      : static_cast<float>(static_cast<const Out*>(a.p.res)[idx]);
-}
-
-template <int MODE>
-__device__ __forceinline__ void store_out(const KArgs& a, int m, int n, float v) {
-  using Out = typename Traits<MODE>::Out;
-  if (a.d.out_f32)
-    static_cast<float*>(a.p.C)[(size_t)m * a.d.ldc + n] = v;
-  else
-    static_cast<Out*>(a.p.C)[(size_t)m * a.d.ldc + n] = static_cast<Out>(v);
-}
-
-template <int MODE>
-__device__ __forceinline__ void epilogue_store(const KArgs& a, int m, int n, float v) {
-  if (a.p.bias) v += a.p.bias[n];
-  if (a.p.res) v += load_res<MODE>(a, m, n);
-  store_out<MODE>(a, m, n, apply_act(v, a.d.act));
 }
 
 __device__ __forceinline__ void split8(const u32x4& x0, const u32x4& x1, half8& hi, half8& lo) {
@@ -162,7 +169,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   int* s_flag = reinterpret_cast<int*>(lds + STAGES * IMG);
 
   const GemmDesc& d = a.d;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
   int tile = blockIdx.x;
   {
@@ -279,41 +287,88 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // Epilogue operands fetched before the first DMAs so their latency hides
-  // under the K loop and the counted vmcnt waits never stall on them (single-
-  // slice tiles only; the split-K reducer reads them itself).  Only small
-  // tiles (16 accumulators per lane) can spare the registers.  The residual is
-  // held in its storage type (Out) and converted in the epilogue: converting
-  // here would force a vmcnt(0) per element.  F16 with an fp32 residual takes
-  // the per-element epilogue.  Out-of-tile lanes read element 0.
-  using Out = typename Traits<MODE>::Out;
-  constexpr bool kPrefetch = TI * TJ <= 4;
-  const bool pre = kPrefetch && gridDim.y == 1 && (sizeof(Out) == 4 || !d.res_f32);
+  // Bias fetched up front (TJ floats; out-of-tile lanes read the zero line).
+  // The residual is NOT prefetched into registers: holding it across the K
+  // loop cost 30-70 VGPRs and a wave per SIMD, which lost 15 % end to end
+  // (34.7k vs 40.9k inf/s, ResNet-18 fp16x3, 4 workers); the epilogue batches
+  // its residual loads once the loop registers are dead instead.
   float bpre[TJ];
-  Out rpre[TI][TJ][4];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int n = n0 + wn * WTN + j * 16 + fr;
-    bpre[j] = (pre && a.p.bias ? a.p.bias : reinterpret_cast<const float*>(zeros))[pre && a.p.bias && n < d.N ? n : 0];
+    bpre[j] = (a.p.bias ? a.p.bias : reinterpret_cast<const float*>(zeros))[a.p.bias && n < d.N ? n : 0];
   }
-  // No branch around the loads (LLVM would sink the conversion into it):
-  // tiles without a residual read the zero line.
-  const bool use_res = pre && a.p.res;
-  const Out* R = use_res ? static_cast<const Out*>(a.p.res) : reinterpret_cast<const Out*>(zeros);
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        const int n = n0 + wn * WTN + j * 16 + fr;
-        rpre[i][j][r] = R[(use_res && m < d.M && n < d.N) ? (size_t)m * d.ldr + n : 0];
-      }
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) issue(s, s);
+
+  // Epilogue, one fragment row-group (i) at a time to bound registers, each in
+  // three branch-free phases (per-element runtime branches made the waitcnt
+  // pass fall back to vmcnt(0) after every store): the group's residual loads
+  // (clamped, always-valid addresses), then bias + residual + activation in
+  // registers (activation chosen once), then the stores (one loop per output
+  // format).
+  auto finish = [&](floatx4 (&v)[TI][TJ]) {
+    using Out = typename TR::Out;
+    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : d.out_f32 ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      float x[TJ][4];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[j][r] = 0.f;
+      if (a.p.res) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+            const int n = n0 + wn * WTN + j * 16 + fr;
+            x[j][r] = load_res<MODE>(a, m < d.M ? m : 0, n < d.N ? n : 0);
+          }
+      }
+      auto apply = [&](auto act_tag) {
+        constexpr Act act = decltype(act_tag)::value;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[j][r] = apply_act(v[i][j][r] + bpre[j] + x[j][r], act);
+      };
+      if (d.act == Act::Relu)
+        apply(std::integral_constant<Act, Act::Relu>{});
+      else if (d.act == Act::Gelu)
+        apply(std::integral_constant<Act, Act::Gelu>{});
+      else
+        apply(std::integral_constant<Act, Act::None>{});
+      auto store_all = [&](auto st) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
+            const int n = n0 + wn * WTN + j * 16 + fr;
+            if (m < d.M && n < d.N) st(m, n, x[j][r]);
+          }
+      };
+      if (fmt == 2) {
+        _Float16* C = static_cast<_Float16*>(a.p.C);
+        store_all([&](int m, int n, float y) {
+          const size_t k = split_idx(m, n, d.ldc);
+          const _Float16 hi = static_cast<_Float16>(y);
+          C[k] = hi;
+          C[k + 32] = static_cast<_Float16>(y - static_cast<float>(hi));
+        });
+      } else if (fmt == 1) {
+        float* C = static_cast<float*>(a.p.C);
+        store_all([&](int m, int n, float y) { C[(size_t)m * d.ldc + n] = y; });
+      } else {
+        Out* C = static_cast<Out*>(a.p.C);
+        store_all([&](int m, int n, float y) { C[(size_t)m * d.ldc + n] = static_cast<Out>(y); });
+      }
+    }
+  };
 
   [[maybe_unused]] unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
   SPI_STAMP(st_t0);
@@ -363,15 +418,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
-    } else if constexpr (MODE == (int)Prec::F16X3) {
+    } else if constexpr (kSplitMode<MODE>) {
       static_assert(ESTEP == 32, "one 32-k block per step");
+      // fp32 A: two 16-byte chunks split into hi/lo below; split A: hi and lo
+      // chunks read like W's (the same conflict-free pattern).
       u32x4 ar0[TI], ar1[TI];
       half8 bh[TJ], bl[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wm * WTM + i * 16 + fr;
-        ar0[i] = rd_chunk<RB>(As, row, 2 * fq);
-        ar1[i] = rd_chunk<RB>(As, row, 2 * fq + 1);
+        ar0[i] = rd_chunk<RB>(As, row, MODE == kF16X3S ? fq : 2 * fq);
+        ar1[i] = rd_chunk<RB>(As, row, MODE == kF16X3S ? 4 + fq : 2 * fq + 1);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
@@ -383,7 +440,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
       SPI_STAMP(st_c);
       half8 ah[TI], al[TI];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) split8(ar0[i], ar1[i], ah[i], al[i]);
+      for (int i = 0; i < TI; ++i) {
+        if constexpr (MODE == kF16X3S) {
+          ah[i] = __builtin_bit_cast(half8, ar0[i]);
+          al[i] = __builtin_bit_cast(half8, ar1[i]);
+        } else {
+          split8(ar0[i], ar1[i], ah[i], al[i]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -448,21 +512,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   }
 #endif
   if (gridDim.y == 1) {
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-          const int n = n0 + wn * WTN + j * 16 + fr;
-          if (m < d.M && n < d.N) {
-            if (pre)
-              store_out<MODE>(a, m, n, apply_act(acc[i][j][r] + bpre[j] + static_cast<float>(rpre[i][j][r]), d.act));
-            else
-              epilogue_store<MODE>(a, m, n, acc[i][j][r]);
-          }
-        }
+    finish(acc);
     return;
   }
 
@@ -492,17 +542,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   }
   __syncthreads();
   if (!*s_flag) return;
-  // Four splits' slabs in flight per round; loads past the last slab fall
+  // Two splits' slabs in flight per round; loads past the last slab fall
   // outside the descriptor's range and return 0 (no branch, no per-load wait).
   floatx4 sum[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int z0 = 0; z0 < splits; z0 += 4) {
-    floatx4 v[4][TI][TJ];
+  for (int z0 = 0; z0 < splits; z0 += 2) {
+    floatx4 v[2][TI][TJ];
 #pragma unroll
-    for (int zz = 0; zz < 4; ++zz)
+    for (int zz = 0; zz < 2; ++zz)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -511,22 +561,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
           v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
         }
 #pragma unroll
-    for (int zz = 0; zz < 4; ++zz)
+    for (int zz = 0; zz < 2; ++zz)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) sum[i][j] += v[zz][i][j];
   }
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        const int n = n0 + wn * WTN + j * 16 + fr;
-        if (m < d.M && n < d.N) epilogue_store<MODE>(a, m, n, sum[i][j][r]);
-      }
+  finish(sum);
 }
 
 struct Plan {
@@ -609,7 +650,7 @@ void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
 
 template <int MODE>
 void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
-  const Plan pl = choose_plan(d, (Prec)MODE);
+  const Plan pl = choose_plan(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE);
   KArgs a{};
   a.d = d;
   a.p = p;
@@ -666,7 +707,12 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
       launch<(int)Prec::F32>(d, p, s);
       break;
     case Prec::F16X3:
-      launch<(int)Prec::F16X3>(d, p, s);
+      // split A relies on one (kh, kw) cell per 32-k step (byte-identical to fp32 addressing)
+      if (d.a_split && d.conv && d.Cin < 32) throw std::invalid_argument("split activations need Cin >= 32");
+      if (d.a_split)
+        launch<kF16X3S>(d, p, s);
+      else
+        launch<(int)Prec::F16X3>(d, p, s);
       break;
   }
 }

@@ -327,6 +327,14 @@ void Model::build_resnet(const PMap& p) {
       if (c->cout && (c->cin_pad % 8 != 0 || (c->cin_pad & (c->cin_pad - 1))))
         throw std::runtime_error("resnet conv channels must be a power of two >= 8");
   }
+  // Split activations need every activation's channel count to be a multiple
+  // of 32 (the split block) and every non-stem conv to read >= 32 channels.
+  split_ = prec_ == Prec::F16X3 && stem_.cout % 32 == 0;
+  for (auto& b : blocks_) {
+    const ConvW* cs[] = {&b.c1, &b.c2, &b.c3, &b.ds};
+    for (const ConvW* c : cs)
+      if (c->cout && (c->cin_pad < 32 || c->cout % 32 != 0)) split_ = false;
+  }
 }
 
 void Model::build_bert(const PMap& p) {
@@ -560,6 +568,8 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   GemmDesc d = conv_desc(c, B, H, W, OH, OW);
   d.act = act;
   d.wplane = c.wplane;
+  d.out_split = split_;
+  d.a_split = split_ && &c != &stem_;  // the stem reads the ingested fp32 image
   const size_t es = f16_ ? 2 : 4;
   if (prof_)
     op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
@@ -725,7 +735,10 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     H = OH;
     const int PH = (H + 2 - 3) / 2 + 1;
     if (prof_) op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
-    maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    if (split_)
+      maxpool_nhwc_split(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, s);
+    else
+      maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
     if (prof_) op_end(s);
     H = PH;
     int cur = 2;
@@ -764,7 +777,10 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       H = H2;
     }
     if (prof_) op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
-    avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+    if (split_)
+      avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
+    else
+      avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const int S = S_in, T = B * S;

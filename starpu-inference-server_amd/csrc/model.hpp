@@ -111,6 +111,9 @@ class Model {
   int family_ = 0;
   Prec prec_ = Prec::F16;
   bool f16_ = true;  // activations stored as fp16 (Prec::F16 only)
+  // ResNet under Prec::F16X3: conv outputs / pool inputs in the split layout
+  // (GemmDesc::a_split), so the GEMM main loop never splits A on the VALU.
+  bool split_ = false;
   int max_batch_ = 1;
   bool graphs_ = false;
   std::string desc_;

@@ -6,6 +6,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -186,6 +187,17 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   auto rt = std::make_unique<spi_runtime>();
   rt->cfg = *c;
   if (rt->cfg.workers_per_device <= 0) rt->cfg.workers_per_device = 4;
+  {
+    // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4)
+    // round-robin; worker streams sharing a queue run serially.
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int queues = q ? std::atoi(q) : 4;
+    if (queues < rt->cfg.workers_per_device + 1)
+      std::fprintf(stderr,
+                   "spi_runtime: GPU_MAX_HW_QUEUES=%d < workers_per_device+1=%d; worker streams will share "
+                   "hardware queues and serialize (set it before the first HIP call)\n",
+                   queues, rt->cfg.workers_per_device + 1);
+  }
   for (int i = 0; i < c->num_inputs; ++i) {
     size_t n = spi_dtype_size(c->input_types[i]);
     if (!n || c->input_ndims[i] < 0 || c->input_ndims[i] >= SPI_MAX_DIMS) return fail("invalid input spec");

@@ -34,6 +34,12 @@ struct GemmDesc {
   Act act = Act::None;
   bool out_f32 = false;  // C is float (else the compute type)
   bool res_f32 = false;  // residual is float (else the compute type)
+  // F16X3 activation split layout: per row, blocks of 32 elements stored as
+  // [32 hi fp16 | 32 lo fp16] (128 bytes, the size of 32 fp32), hi = fp16(x),
+  // lo = fp16(x - hi).  a_split: A and the residual are split (conv Cin >= 32);
+  // out_split: C is written split.
+  bool a_split = false;
+  bool out_split = false;
 };
 
 struct GemmPtrs {
@@ -63,6 +69,11 @@ void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH,
 // Global average pool NHWC [B,HW,C] -> [B,C] (compute type).
 void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16,
                   hipStream_t s);
+// The same two on F16X3 split activations (GemmDesc::a_split layout, C % 32 == 0):
+// max pool split -> split, average pool split -> fp32 [B,C].
+void maxpool_nhwc_split(const void* x, void* y, int B, int H, int W, int C, int OH,
+                        int OW, int k, int stride, int pad, hipStream_t s);
+void avgpool_nhwc_split(const void* x, float* y, int B, int HW, int C, hipStream_t s);
 // Row LayerNorm over D: y = LN(x) * g + b.  x fp32 [rows, ldx]; writes fp32
 // (yf, may alias x) and/or compute-type (yt) outputs.
 void layernorm(const float* x, int ldx, const float* g, const float* b,

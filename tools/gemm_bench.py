@@ -26,9 +26,22 @@ GEMMS = [("bert_qkv", 1024, 2304, 768), ("bert_out", 1024, 768, 768), ("bert_ff1
          ("vit_ff2", 3152, 1024, 4096), ("sq4096", 4096, 4096, 4096)]
 
 
+EAGER = False
+
+
 def timeit(fn, reps):
-    """Device time per launch: `reps` launches captured in one graph, replayed."""
+    """Device time per launch: `reps` launches captured in one graph, replayed
+    (--eager: plain launches, for PMC profiling)."""
     fn()
+    if EAGER:
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
@@ -51,7 +64,10 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
     ap.add_argument("--plans", default="", help="';'-separated SPI_GEMM_PLAN values to sweep ('' = the chooser)")
+    ap.add_argument("--eager", action="store_true")
     a = ap.parse_args()
+    global EAGER
+    EAGER = a.eager
     plans = a.plans.split(";") if a.plans else [""]
 
     def sweep(fn, label, fl):
