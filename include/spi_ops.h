@@ -37,8 +37,8 @@ int spi_op_gemm(int32_t precision, const void* A, int32_t M, int32_t K, int32_t 
                 int32_t res_f32, int32_t ldr, void* C, int32_t out_f32, int32_t ldc,
                 int32_t act, void* workspace, void* stream);
 
-/* NHWC conv as implicit GEMM: x [B][H][W][Cin] (Cin a power of two >= 8,
- * >= 4 for fp32), W packed from [Cout][KH][KW][Cin] order, y [B][OH][OW][Cout]. */
+/* NHWC conv as implicit GEMM: x [B][H][W][Cin] (Cin a power of two >= 8 for fp16,
+ * >= 4 for fp32 / fp16x3), W packed from [Cout][KH][KW][Cin] order, y [B][OH][OW][Cout]. */
 int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_t W,
                   int32_t Cin, const void* W_packed, int32_t Cout, int32_t KH, int32_t KW,
                   int32_t stride, int32_t pad, const float* bias, const void* residual,

@@ -293,7 +293,9 @@ void Model::build_resnet(const PMap& p) {
   // Stages: torchvision layer1..layer4, stride 2 on the first block of 2..4
   // (on conv1 for BasicBlock, conv2 for Bottleneck: torchvision v1.5).
   bottleneck_ = has(p, "layer1.0.conv3.weight");
-  const int cin_pad = prec_ == Prec::F32 ? 4 : 8;
+  // Stem input channels padded to one 16-byte chunk per pixel: 4 fp32
+  // (F32, and F16X3 whose A is fp32) or 8 fp16 (F16).
+  const int cin_pad = prec_ == Prec::F16 ? 8 : 4;
   stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, prec_, eps_);
   if (stem_.kh != 7 || stem_.cin != 3) throw std::runtime_error("resnet stem must be 7x7 over 3 channels");
   for (int L = 1; L <= 4; ++L) {

@@ -102,7 +102,7 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
                   int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, const float* bias,
                   const void* residual, void* y, int32_t act, void* workspace, void* stream) {
   spi::Prec p;
-  const int min_cin = precision == 0 ? 4 : 8;
+  const int min_cin = precision == 1 ? 8 : 4;  // one 16-byte chunk: 8 fp16 or 4 fp32
   if (!prec_of(precision, &p) || !x || !Wp || !y || !workspace || B <= 0 || Cin < min_cin ||
       (Cin & (Cin - 1)) || Cout <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0 || act < 0 || act > 2)
     return fail("invalid conv arguments");

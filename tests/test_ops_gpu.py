@@ -63,7 +63,7 @@ def test_conv2d_nhwc(ops, prec, B, H, cin, cout, k, stride):
     w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
     b = torch.randn(cout, generator=g)
     pad = k // 2
-    cin_pad = max(cin, 4 if prec == "fp32" else 8)
+    cin_pad = max(cin, 8 if prec == "fp16" else 4)
     dt = ops.act_dtype(prec)
     x_nhwc = torch.zeros(B, H, H, cin_pad)
     x_nhwc[..., :cin] = x.permute(0, 2, 3, 1)
