@@ -155,8 +155,20 @@ __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
   return *reinterpret_cast<const u32x4*>(img + row * RB + ((c ^ (row & (CPR - 1))) << 4));
 }
 
+// Split-K is compiled into the 64x64 tiles only (no plan rule splits a larger
+// tile; its reducer alone cost 36-120 VGPRs there).  Launch bounds ask for the
+// occupancy each tile reaches within its registers: 4 / 3 / 2 waves per SIMD.
+template <int BM, int BN>
+constexpr bool kSplitK = BM == 64 && BN == 64;
+// Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
+// size, capped by what the tile's LDS ring allows (one wave per SIMD per block,
+// 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
+template <int BM, int BN, int STAGES>
+constexpr int kMinWaves = std::min(BM * BN <= 64 * 64 ? 4 : BM * BN <= 128 * 64 ? 3 : 2,
+                                   (160 * 1024) / (STAGES * (BM + BN) * 128 + 16));
+
 template <int MODE, int BM, int BN, int STAGES, bool CONV>
-__global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
+__global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(KArgs a) {
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
@@ -511,10 +523,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
     g[4] = (unsigned long long)nsteps;
   }
 #endif
-  if (gridDim.y == 1) {
+  if (!kSplitK<BM, BN> || gridDim.y == 1) {
     finish(acc);
     return;
   }
+  if constexpr (kSplitK<BM, BN>) {
 
   // ---- split-K: publish this slice's slab, the last arriver reduces -------
   // Slabs are written in fragment order (thread tid's accumulator (i, j) is 16
@@ -568,6 +581,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
         for (int j = 0; j < TJ; ++j) sum[i][j] += v[zz][i][j];
   }
   finish(sum);
+  }
 }
 
 struct Plan {
@@ -579,59 +593,92 @@ int estep_of(Prec prec) {
                            : prec == Prec::F32 ? Traits<(int)Prec::F32>::ESTEP : Traits<(int)Prec::F16X3>::ESTEP;
 }
 
-// Tuning hook: SPI_GEMM_PLAN="bm,bn,stages,splits" forces the plan (micro-benchmarks
-// only; read on every call so a sweep can change it in-process).
-bool plan_override(Plan* pl) {
-  const char* env = std::getenv("SPI_GEMM_PLAN");
-  if (!env || !*env) return false;
-  int bm = 0, bn = 0, st = 0, sp = 0;
-  if (std::sscanf(env, "%d,%d,%d,%d", &bm, &bn, &st, &sp) != 4) return false;
-  const bool ok_tile = (bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64);
-  const bool ok_st = st >= 2 && st <= 4 && !(bm == 128 && bn == 128 && st > 2) && !(bm == 128 && bn == 64 && st > 3);
-  if (!ok_tile || !ok_st || sp < 1) return false;
-  *pl = Plan{bm, bn, st, sp, 0};
-  return true;
+// Tuning knobs, read once (getenv on every launch cost ~0.5 us each, and the
+// plan is evaluated three times per launch); spi_debug_gemm_reload_env()
+// re-reads them for in-process sweeps (tools/gemm_bench.py).
+//   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM
+//   SPI_GEMM_POLICY=latency | tput:T      plan rule (default tput:192)
+//   SPI_GEMM_MAXSPLIT=S, SPI_GEMM_STAGES=N  caps for experiments
+struct Knobs {
+  bool forced = false;
+  Plan plan{};
+  bool latency = false;
+  int target = 192;
+  int max_split = 0, stages = 0;
+};
+
+Knobs read_knobs() {
+  Knobs k;
+  if (const char* e = std::getenv("SPI_GEMM_PLAN"); e && *e) {
+    int bm = 0, bn = 0, st = 0, sp = 0;
+    if (std::sscanf(e, "%d,%d,%d,%d", &bm, &bn, &st, &sp) == 4) {
+      const bool ok_tile = (bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64);
+      const bool ok_st = st >= 2 && st <= 4 && !(bm == 128 && bn == 128 && st > 2) && !(bm == 128 && bn == 64 && st > 3);
+      if (ok_tile && ok_st && sp >= 1) {
+        k.forced = true;
+        k.plan = Plan{bm, bn, st, sp, 0};
+      }
+    }
+  }
+  if (const char* e = std::getenv("SPI_GEMM_POLICY"); e && *e) {
+    if (std::strcmp(e, "latency") == 0) k.latency = true;
+    if (std::strncmp(e, "tput:", 5) == 0) k.target = std::max(1, std::atoi(e + 5));
+  }
+  if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SPI_GEMM_STAGES"); e && *e) k.stages = std::max(2, std::min(4, std::atoi(e)));
+  return k;
 }
 
+Knobs& knobs() {
+  static Knobs k = read_knobs();
+  return k;
+}
+
+Plan finish_plan(Plan pl, int ksteps, int ES) {
+  const Knobs& k = knobs();
+  if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
+  if (pl.bm != 64 || pl.bn != 64) pl.splits = 1;  // split-K exists in the 64x64 kernels only
+  if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
+  pl.splits = std::max(1, std::min(pl.splits, ksteps));
+  const int kt = (ksteps + pl.splits - 1) / pl.splits;
+  pl.k_per_split = kt * ES;
+  pl.splits = (ksteps + kt - 1) / kt;
+  return pl;
+}
+
+// Plan rule (default): the largest tile that still yields >= T workgroups,
+// split-K only when even 64x64 tiles fall short (then to ~T workgroups, >= 6
+// k-steps per slice).  T = 192 measured best with 4 concurrent worker streams
+// (ResNet-18 bs8 fp16x3 +8 %, ResNet-152 bs32 +8 %, BERT-base +5 %, ViT-L +7 %
+// over the latency rule; tools/gemm_bench.py / bench.py sweeps).
+// SPI_GEMM_POLICY=latency keeps the single-stream rule: 64x64 tiles and
+// split-K to ~2 workgroups per CU.
 Plan choose_plan(const GemmDesc& d, Prec prec) {
-  constexpr int kTarget = 256;  // CUs
+  const Knobs& k = knobs();
   const int ES = estep_of(prec);
   const int ksteps = d.Kpad / ES;
-  Plan forced;
-  if (plan_override(&forced)) {
-    const int sp = std::min(forced.splits, ksteps);
-    const int kt_per = (ksteps + sp - 1) / sp;
-    forced.k_per_split = kt_per * ES;
-    forced.splits = (ksteps + kt_per - 1) / kt_per;
-    return forced;
-  }
-  // Measured on ResNet-18 / BERT-base / ViT-L layer shapes (tools/gemm_bench.py
-  // --plans): 64x64 tiles win unless the grid is very large; what small-M
-  // layers need is more workgroups per CU, which split-K supplies.
+  if (k.forced) return finish_plan(k.plan, ksteps, ES);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
-  if (const char* pol = std::getenv("SPI_GEMM_POLICY"); pol && std::strncmp(pol, "tput:", 5) == 0) {
-    // Experiment: largest tile with >= T tiles, no split-K unless 64x64 falls short.
-    const int T = std::max(1, std::atoi(pol + 5));
-    if (d.N > 64 && tiles_of(128, 128) >= T) return Plan{128, 128, 2, 1, d.Kpad};
-    if (tiles_of(128, 64) >= T) return Plan{128, 64, ksteps >= 16 ? 3 : 2, 1, d.Kpad};
+  const auto stages_for = [](int kt) { return kt >= 16 ? 3 : 2; };  // a deeper ring pays only on long K loops
+  if (!k.latency) {
+    const int T = k.target;
+    if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES);
+    if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES);
     const int t64 = tiles_of(64, 64);
     const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
-    const int kt = (ksteps + sp - 1) / sp;
-    return Plan{64, 64, kt >= 16 ? 3 : 2, (ksteps + kt - 1) / kt, kt * ES};
+    return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES);
   }
-  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return Plan{128, 128, 2, 1, d.Kpad};
-  if (prec == Prec::F16 && tiles_of(128, 64) >= 384 && ksteps >= 32) return Plan{128, 64, 3, 1, d.Kpad};
+  constexpr int kTarget = 256;  // CUs
+  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES);
+  if (prec == Prec::F16 && tiles_of(128, 64) >= 384 && ksteps >= 32)
+    return finish_plan(Plan{128, 64, 3, 1, 0}, ksteps, ES);
   const int tiles = tiles_of(64, 64);
   int splits = 1;
   if (tiles < kTarget) {
     const int want = (prec == Prec::F16 ? 384 : 512) / tiles;  // workgroups per launch
     splits = std::max(1, std::min(want, ksteps / 6));            // >= 6 k-steps per slice
   }
-  const int kt_per = (ksteps + splits - 1) / splits;
-  Plan pl{64, 64, kt_per >= 16 ? 3 : 2, 1, 0};  // a deeper ring pays only on long K loops
-  pl.k_per_split = kt_per * ES;
-  pl.splits = (ksteps + kt_per - 1) / kt_per;
-  return pl;
+  return finish_plan(Plan{64, 64, stages_for((ksteps + splits - 1) / splits), splits, 0}, ksteps, ES);
 }
 
 int ilog2(int v) {
@@ -691,6 +738,8 @@ size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
 }
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }
+
+extern "C" void spi_debug_gemm_reload_env(void) { knobs() = read_knobs(); }
 
 #ifdef SPI_GEMM_STAMPS
 extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {

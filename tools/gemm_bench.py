@@ -73,6 +73,7 @@ def main():
     def sweep(fn, label, fl):
         for plan in plans:
             os.environ["SPI_GEMM_PLAN"] = plan
+            ops.lib.spi_debug_gemm_reload_env()  # knobs are cached in the library
             try:
                 ms = timeit(fn, a.reps)
             except ops.OpError as e:
@@ -80,6 +81,7 @@ def main():
                 continue
             print(f"{label}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s  [{plan or 'auto'}]", flush=True)
         os.environ["SPI_GEMM_PLAN"] = ""
+        ops.lib.spi_debug_gemm_reload_env()
     dt = ops.act_dtype(a.prec)
     ws = ops.workspace()
     rng = np.random.default_rng(0)
