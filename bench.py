@@ -45,6 +45,7 @@ WORKLOADS = {
     "vit_l_16": "ViT-L/16 224^2 bs=16 fp16 (patch-embed GEMM + MFMA attention, LDS-tiled)",
 }
 PEAK_TFLOPS = {"fp16": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
 
 
 def percentile(samples, p):
@@ -91,7 +92,7 @@ def make_inputs(name, batch, rng, seq=128):
 class Harness:
     """Prebuilt codelet calls (cl_arg + buffers + stream) for `workers` workers of one device."""
 
-    def __init__(self, spi, replica, name, dev, batch, workers, rng):
+    def __init__(self, spi, replica, name, dev, batch, workers, rng, streams=None):
         import torch
 
         self.spi, self.lib, self.N = spi, spi.lib, spi._native
@@ -99,7 +100,9 @@ class Harness:
         self.dev = dev
         self.replica = replica
         self.batch = batch
-        self.streams = [torch.cuda.Stream(dev) for _ in range(workers)]
+        # Reuse the worker streams of an earlier harness when given: each new HIP
+        # stream takes a hardware queue, and queues beyond GPU_MAX_HW_QUEUES are shared.
+        self.streams = list(streams) if streams is not None else [torch.cuda.Stream(dev) for _ in range(workers)]
         self.host_inputs, self.out_shape = make_inputs(name, batch, rng)
         self.d_in = [[torch.from_numpy(x).to(dev) for x in self.host_inputs] for _ in range(workers)]
         self.d_out = [torch.empty(self.out_shape, device=dev, dtype=torch.float32) for _ in range(workers)]
@@ -178,23 +181,46 @@ class Harness:
                 out.append((time.perf_counter() - ts) * 1e3)
         return out
 
-    def dominant_kernel(self, precision):
+    def dominant_kernel(self, precision, model=""):
         ops = self.replica.profile(self.d_in[0], self.d_out[0], self.streams[0].cuda_stream)
         totals = {}
         for op in ops:
             t = totals.setdefault(op["name"], [0.0, 0, op["flops"], op["bytes"]])
             t[0] += op["ms"]
             t[1] += 1
-        name, (tot, cnt, flops, _bytes) = max(totals.items(), key=lambda kv: kv[1][0])
+        name, (tot, cnt, flops, nbytes) = max(totals.items(), key=lambda kv: kv[1][0])
         ms = tot / cnt
-        peak = PEAK_TFLOPS[precision]
-        ach = flops / (ms * 1e-3) / 1e12
         fwd_ms = sum(o["ms"] for o in ops)
         fwd_flops = sum(o["flops"] for o in ops)
-        return {"bound": "mfma", "kernel": name, "launches_per_forward": cnt, "achieved": round(ach, 3),
-                "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 5), "traffic": None,
-                "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(ms, 5),
-                "forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5)}
+        peak = PEAK_TFLOPS[precision]
+        traffic, src = measured_traffic(model, self.batch, precision, name)
+        common = {"kernel": name, "launches_per_forward": cnt, "traffic": traffic, "traffic_source": src,
+                  "avg_launch_ms": round(ms, 5), "forward_share": round(tot / fwd_ms, 4),
+                  "forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5)}
+        if flops == 0:  # a byte-moving op dominates: HBM roofline on its algorithmic bytes
+            ach = nbytes / (ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(ach / PEAK_HBM_GBS, 5), "algorithmic_bytes_per_launch": nbytes, **common}
+        ach = flops / (ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 5), "algorithmic_flops_per_launch": flops,
+                "mfma_issue_per_flop": 3 if precision == "fp16x3" else 1, **common}
+
+
+def measured_traffic(model, batch, precision, op):
+    """HBM bytes per launch of `op` from the committed PMC profile
+    profiles/<round>/traffic_<model>_bs<batch>_<precision>.json (tools/pmc_traffic.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction), or None."""
+    import glob
+
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{model}_bs{batch}_{precision}.json")))
+    if not hits:
+        return None, None
+    with open(hits[-1]) as f:
+        ops = json.load(f).get("ops", {})
+    if op not in ops:
+        return None, None
+    return ops[op]["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
 
 
 def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4):
@@ -246,9 +272,11 @@ def main():
     # One HIP hardware queue per worker stream: HIP maps streams onto
     # GPU_MAX_HW_QUEUES queues round-robin (default 4, shared with torch's own
     # streams), and worker streams that share a queue run serially -- measured
-    # 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues.  Must be set
-    # before the first HIP call.
-    queues = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), args.workers + 4))
+    # 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues (16 measured
+    # the same as 8).  Room for two sets of worker streams: the harness's and the
+    # mini-runtime extra's own.  Must be set before the first HIP call (DESIGN.md,
+    # INTEGRATION.md).
+    queues = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 2 * args.workers + 4))
     os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -310,7 +338,7 @@ def main():
         result["e2e_inferences_per_s_serial"] = round(args.batch / (percentile(e2e, 50) * 1e-3), 2)
         result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
         result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
-        result["roofline"] = h.dominant_kernel(args.precision)
+        result["roofline"] = h.dominant_kernel(args.precision, args.model)
 
     if rank == 0 and args.cpu_seconds > 0:
         from oracle.cpu_codelet import cpu_inference
@@ -333,14 +361,14 @@ def main():
         extras = {}
         # plain fp16 operands on the same workload (faster, 1.8e-3 parity on this network)
         r16 = spi.ModelReplica(model, dev, "fp16", max_batch=args.batch, graphs=True)
-        h16 = Harness(spi, r16, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1))
+        h16 = Harness(spi, r16, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
         el, lat = h16.throughput(args.steps, args.warmup)
         extras["resnet18_bs8_fp16_plain"] = {
             "value": round(args.workers * args.batch * args.steps / el, 2), "unit": "inferences/s",
             "p50_task_latency_ms": round(percentile(lat, 50), 4), "parity_normalised_max_err": 1.8e-3}
         # ResNet-18 bs=1 latency (the metric names it)
         r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
-        h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2))
+        h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2), h.streams)
         el, lat = h1.throughput(args.steps, args.warmup)
         e2e1 = h1.serial_e2e(args.latency_iters)
         extras["resnet18_bs1"] = {"value": round(args.workers * args.steps / el, 2), "unit": "inferences/s",
@@ -353,14 +381,14 @@ def main():
         # BERT-base seq128 bs8 fp16 (BASELINE configs[2])
         bmodel = zoo.build("bert_base", seed=0)
         rb = spi.ModelReplica(bmodel, dev, "fp16", max_batch=8, seq_len=seq, graphs=True)
-        hb = Harness(spi, rb, "bert_base", dev, 8, args.workers, np.random.default_rng(3))
+        hb = Harness(spi, rb, "bert_base", dev, 8, args.workers, np.random.default_rng(3), h.streams)
         el, lat = hb.throughput(max(20, args.steps // 4), 5)
         e2eb = hb.serial_e2e(10)
         extras["bert_base_seq128_bs8_fp16"] = {
             "value": round(args.workers * 8 * max(20, args.steps // 4) / el, 2), "unit": "sequences/s",
             "p50_task_latency_ms": round(percentile(lat, 50), 4),
             "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2eb, 50), 4),
-            "gflop_per_seq": round(rb.flops(1) / 1e9, 3), "roofline": hb.dominant_kernel("fp16")}
+            "gflop_per_seq": round(rb.flops(1) / 1e9, 3), "roofline": hb.dominant_kernel("fp16", "bert_base")}
         result["extras"] = extras
 
     if world > 1:

@@ -719,13 +719,19 @@ void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStrea
     ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
-    bert_embed(static_cast<const int64_t*>(in[0]), ptr<float>(word_), ptr<float>(pos_), ptr<float>(type0_),
-               ptr<float>(emb_ln_.g), ptr<float>(emb_ln_.b), static_cast<float*>(w.bufs[0]),
-               f16_ ? w.bufs[1] : nullptr, B, S, D_, vocab_, eps_, f16_, s);
+    const double T = (double)B * S;
+    prof_op(s, "bert_embed", T * D_ * (4 * 3 + 4 + (f16_ ? 2 : 0)), [&] {
+      bert_embed(static_cast<const int64_t*>(in[0]), ptr<float>(word_), ptr<float>(pos_), ptr<float>(type0_),
+                 ptr<float>(emb_ln_.g), ptr<float>(emb_ln_.b), static_cast<float*>(w.bufs[0]),
+                 f16_ ? w.bufs[1] : nullptr, B, S, D_, vocab_, eps_, f16_, s);
+    });
     w.has_mask = in[1] != nullptr;
-    if (w.has_mask) mask_to_bias(static_cast<const int64_t*>(in[1]), w.mask_bias, B * S, s);
+    if (w.has_mask)
+      prof_op(s, "mask_to_bias", T * 12,
+              [&] { mask_to_bias(static_cast<const int64_t*>(in[1]), w.mask_bias, B * S, s); });
   } else if (family_ == SPI_FAMILY_VIT) {
-    patchify(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, patch_, f16_, s);
+    prof_op(s, "patchify", (double)B * 3 * image_ * image_ * (4 + (f16_ ? 2 : 4)),
+            [&] { patchify(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, patch_, f16_, s); });
   }
 }
 
@@ -800,12 +806,16 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
       run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s);
-      layernorm(a, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_, s);
+      prof_op(s, "layernorm", ln_bytes(T, true), [&] {
+        layernorm(a, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_, s);
+      });
       run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w, s);
       run_gemm(L.ff2, ff, T, ffn_, a, D_, true, Act::None, hf, true, D_, w, s);
       if (i + 1 < layers_)
-        layernorm(a, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_,
-                  s);
+        prof_op(s, "layernorm", ln_bytes(T, true), [&] {
+          layernorm(a, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_,
+                    s);
+        });
     }
   } else if (family_ == SPI_FAMILY_VIT) {
     const int S = npatch_ + 1, T = B * S;
@@ -813,24 +823,32 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     float* x = static_cast<float*>(buf[2]);
     run_gemm(patch_proj_, buf[0], B * npatch_, patch_proj_.k, buf[1], D_, true, Act::None, nullptr, false, 0,
              w, s);
-    vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
+    prof_op(s, "vit_assemble", (double)T * D_ * 4 * 3, [&] {
+      vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
+    });
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     for (const TfLayer& L : tf_) {
-      layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
-                f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      prof_op(s, "layernorm", ln_bytes(T, false), [&] {
+        layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
+                  f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      });
       run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s);
       if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
       attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
       run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s);
-      layernorm(x, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
-                f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      prof_op(s, "layernorm", ln_bytes(T, false), [&] {
+        layernorm(x, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
+                  f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
+      });
       run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s);
       run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w, s);
     }
     // final LN on the class-token rows only (torchvision: x = ln(x); x = x[:, 0])
-    layernorm(x, S * D_, ptr<float>(final_ln_.g), ptr<float>(final_ln_.b),
-              f16_ ? nullptr : static_cast<float*>(buf[7]), f16_ ? buf[7] : nullptr, D_, B, D_, eps_, f16_, s);
+    prof_op(s, "layernorm_cls", ln_bytes(B, false), [&] {
+      layernorm(x, S * D_, ptr<float>(final_ln_.g), ptr<float>(final_ln_.b),
+                f16_ ? nullptr : static_cast<float*>(buf[7]), f16_ ? buf[7] : nullptr, D_, B, D_, eps_, f16_, s);
+    });
   }
 }
 
@@ -840,8 +858,10 @@ void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s
   } else if (family_ == SPI_FAMILY_BERT) {
     const TfLayer& L = tf_.back();
     const int T = B * S;
-    layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
-              static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
+    prof_op(s, "layernorm_out", (double)T * D_ * 8, [&] {
+      layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
+                static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
+    });
   } else if (family_ == SPI_FAMILY_VIT) {
     run_gemm(head_, w.bufs[7], B, D_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);
   }

@@ -146,6 +146,17 @@ class Model {
   std::vector<OpRecord>* prof_ = nullptr;  // set only inside profile()
   void op_begin(hipStream_t s, const std::string& name, double flops, double bytes);
   void op_end(hipStream_t s);
+  // Profiled launch (bytes = algorithmic traffic); a plain call when not profiling.
+  template <typename F>
+  void prof_op(hipStream_t s, const char* name, double bytes, F&& launch) {
+    if (prof_) op_begin(s, name, 0, bytes);
+    launch();
+    if (prof_) op_end(s);
+  }
+  // LayerNorm over rows x D_: fp32 in + fp32 out (+ compute-type copy).
+  double ln_bytes(double rows, bool f32_out) const {
+    return rows * D_ * (4 + (f32_out ? 4 : 0) + (f16_ ? 2 : (f32_out ? 0 : 4)));
+  }
 
   friend struct Workspace;
 };

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--graphs", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--analyze", default="")
+    ap.add_argument("--ops-out", default="", help="write the forward's op names (launch order) to this JSON file")
     a = ap.parse_args()
     if a.analyze:
         analyze(a.analyze)
@@ -69,8 +70,13 @@ def main():
     zoo = importlib.import_module("starpu-inference-server_amd.zoo")
     m = zoo.build(a.model)
     rep = spi.ModelReplica(m, 0, a.precision, max_batch=a.batch, seq_len=128 if a.model.startswith("bert") else 0)
-    rep.set_graphs(bool(a.graphs))
     h = bench.Harness(spi, rep, a.model, 0, a.batch, 1, np.random.default_rng(0))
+    if a.ops_out:  # op names in launch order (one eager profiled forward; tools/pmc_traffic.py maps dispatches)
+        import json
+        ops = rep.profile(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream)
+        with open(a.ops_out, "w") as f:
+            json.dump([o["name"] for o in ops], f)
+    rep.set_graphs(bool(a.graphs))
     for _ in range(a.iters):
         torch.cuda.synchronize()
         time.sleep(0.001)
