@@ -167,8 +167,15 @@ template <int BM, int BN, int STAGES>
 constexpr int kMinWaves = std::min(BM * BN <= 64 * 64 ? 4 : BM * BN <= 128 * 64 ? 3 : 2,
                                    (160 * 1024) / (STAGES * (BM + BN) * 128 + 16));
 
-template <int MODE, int BM, int BN, int STAGES, bool CONV>
+// A-operand kinds: dense rows; conv with one (kh, kw) tap per k-step (Cin >= the
+// k-step: scalar tap walk + per-row tap mask); conv in general (per-chunk taps:
+// the stem).  Separate instantiations keep each kind's loop free of the others.
+enum : int { kDense = 0, kConvTap = 1, kConvGen = 2 };
+
+template <int MODE, int BM, int BN, int STAGES, int KIND>
 __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(KArgs a) {
+  constexpr bool CONV = KIND != kDense;
+  constexpr bool TAP = KIND == kConvTap;
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
@@ -205,6 +212,10 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   bool a_ok[AQ];
   const AT* a_base[AQ];
   const AT* a_pix[AQ];  // conv: image pointer at (ih0, iw0), may point before the image
+  const AT* a_src[AQ];  // conv, one tap per step: a_pix + this lane's chunk offset
+  // conv, one tap per step: bit (kh*KW + kw) set when that tap of this row lies
+  // inside the image (0 for rows past M).  Indexed by the unrolled q only.
+  uint32_t a_mask[AQ];
 #pragma unroll
   for (int q = 0; q < AQ; ++q) {
     const int r = (wave * AQ + q) * RPI + lane / CPR;
@@ -222,10 +233,21 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       a_iw0[q] = ow * d.stride - d.pad;
       a_base[q] = Ap + (size_t)img * d.H * d.W * d.Cin;
       a_pix[q] = a_base[q] + ((ptrdiff_t)(a_ih0[q] * d.W + a_iw0[q]) << a.cin_shift);
+      a_src[q] = a_pix[q] + a_koff[q];
+      uint32_t mask = 0u;
+      if (TAP && a_ok[q])
+        for (int kh = 0; kh < d.KH; ++kh)
+          for (int kw = 0; kw < d.KW; ++kw) {
+            const int ih = a_ih0[q] + kh, iw = a_iw0[q] + kw;
+            if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W) mask |= 1u << (kh * d.KW + kw);
+          }
+      a_mask[q] = mask;
     } else {
       a_ih0[q] = a_iw0[q] = 0;
       a_base[q] = Ap + (size_t)mm * d.lda;
       a_pix[q] = a_base[q];
+      a_src[q] = a_pix[q];
+      a_mask[q] = 0u;
     }
   }
   const char* b_src[BQ];
@@ -238,23 +260,44 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     b_src[q] = Wb + (size_t)(n0 + r) * row_bytes + c * 16;
   }
 
+  // Cin >= k-step (one (kh, kw) tap per step): a scalar walk over (tap, channel
+  // block), advanced once per issued step (issue() is called for steps 0, 1, 2 ...
+  // in order): cu_cell = tap index, cu_off = element offset of (kh, kw, channel)
+  // from the row's (ih0, iw0) pixel.  Taps past KH*KW (the Kpad tail) have no
+  // mask bit, so they read zeros.
+  int cu_cell = 0, cu_kw = 0, cu_ci = 0, cu_off = 0;
+  if constexpr (TAP) {
+    {
+      cu_cell = kbeg >> a.cin_shift;
+      const int kh = (cu_cell * a.kw_mul) >> 16;
+      cu_kw = cu_cell - kh * d.KW;
+      cu_ci = kbeg & (d.Cin - 1);
+      cu_off = ((kh * d.W + cu_kw) << a.cin_shift) + cu_ci;
+    }
+  }
+  int w_kb = (kbeg / ESTEP) * RB;  // W byte offset of the next issued step
   auto issue = [&](int step, int stage) {
     const int k0 = kbeg + step * ESTEP;
     char* dst = lds + stage * IMG;
     if constexpr (CONV) {
-      if (a.cell_uniform) {
-        // Cin >= k-step: the whole step sits in one (kh, kw) cell -> scalar math.
-        const int cell = k0 >> a.cin_shift;
-        const int kh = (cell * a.kw_mul) >> 16;
-        const int kw = cell - kh * d.KW;
-        const ptrdiff_t step_off = ((ptrdiff_t)(kh * d.W + kw) << a.cin_shift) + (k0 & (d.Cin - 1));
-        const bool k_ok = k0 < d.K;
+      if constexpr (TAP) {
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
-          const int ih = a_ih0[q] + kh, iw = a_iw0[q] + kw;
-          const bool ok = k_ok && a_ok[q] && (unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W;
-          const char* src = ok ? reinterpret_cast<const char*>(a_pix[q] + step_off + a_koff[q]) : zeros;
+          const bool ok = (a_mask[q] >> cu_cell) & 1u;
+          const char* src = ok ? reinterpret_cast<const char*>(a_src[q] + cu_off) : zeros;
           __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+        }
+        // advance one k-step: next channel block, or the next tap (next pixel,
+        // or the next filter row: W - KW + 1 pixels on)
+        cu_ci += ESTEP;
+        cu_off += ESTEP;
+        if (cu_ci == d.Cin) {
+          cu_ci = 0;
+          ++cu_cell;
+          if (++cu_kw == d.KW) {
+            cu_kw = 0;
+            cu_off += (d.W - d.KW) << a.cin_shift;
+          }
         }
       } else {
 #pragma unroll
@@ -281,12 +324,12 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
-    // k-step byte offset inside a W row: RB bytes per step.
-    const size_t kb = (size_t)(k0 / ESTEP) * RB;
+    // k-step byte offset inside a W row: RB bytes per step (advanced per issue).
 #pragma unroll
     for (int q = 0; q < BQ; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[q] + kb),
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[q] + w_kb),
                                        (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
+    w_kb += RB;
   };
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -384,7 +427,11 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
 
   [[maybe_unused]] unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
   SPI_STAMP(st_t0);
-  for (int t = 0; t < nsteps; ++t) {
+  // One k-step; U = t % STAGES is a compile-time constant (the loop below is
+  // unrolled by STAGES), so every stage offset -- M0 of the DMAs, the base of
+  // the fragment reads -- is an immediate.
+  auto kstep = [&](int t, auto u_arg) {
+    const int U = u_arg;  // a constant when u_arg is a std::integral_constant
     SPI_STAMP(st_a);
     // Step t has landed once at most (issued steps after t) DMA groups remain.
     if constexpr (STAGES == 4) {
@@ -405,10 +452,10 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     SPI_STAMP(st_b);
     // All of this step's fragment reads go out first, then the next step's
     // DMAs (their issue cost overlaps the LDS latency), then the MFMAs.
-    const char* As = lds + (t % STAGES) * IMG;
+    const char* As = lds + U * IMG;
     const char* Bs = As + BM * RB;
     auto issue_next = [&] {
-      if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
     };
     if constexpr (MODE == (int)Prec::F16) {
       half8 af[2][TI], bf[2][TJ];
@@ -510,6 +557,28 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     st_wait += st_b - st_a;
     st_issue += st_c - st_b;
     st_comp += st_d - st_c;
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  if constexpr (TAP) {
+    // unrolled by STAGES: stage offsets are immediates (the conv loop is short;
+    // unrolling the large dense-GEMM bodies measured 1-2 % slower end to end)
+    int t = 0;
+    for (; t + STAGES <= nsteps; t += STAGES) {
+      kstep(t, I0{});
+      kstep(t + 1, I1{});
+      if constexpr (STAGES > 2) kstep(t + 2, I2{});
+      if constexpr (STAGES > 3) kstep(t + 3, I3{});
+    }
+    if (t < nsteps) kstep(t, I0{});
+    if constexpr (STAGES > 2)
+      if (t + 1 < nsteps) kstep(t + 1, I1{});
+    if constexpr (STAGES > 3)
+      if (t + 2 < nsteps) kstep(t + 2, I2{});
+  } else {
+    for (int t = 0; t < nsteps; ++t) kstep(t, t % STAGES);
   }
 
   SPI_STAMP(st_d);
@@ -689,10 +758,14 @@ int ilog2(int v) {
 
 template <int MODE, int BM, int BN, int STAGES>
 void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
-  if (a.d.conv)
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, true>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, false>), grid, dim3(256), 0, s, a);
+  if (a.cell_uniform) {
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvTap>), grid, dim3(256), 0, s, a);
+  } else if (a.d.conv) {
+    if constexpr (MODE != kF16X3S)  // split A needs one tap per step (checked in gemm())
+      hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvGen>), grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kDense>), grid, dim3(256), 0, s, a);
+  }
 }
 
 template <int MODE>
@@ -706,7 +779,8 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.tiles = a.tiles_m * ((d.N + pl.bn - 1) / pl.bn);
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
-  a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP;
+  // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
+  a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP && d.KH * d.KW <= 31;
   const dim3 grid(a.tiles, pl.splits);
   if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(a, grid, s);
@@ -757,7 +831,8 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
       break;
     case Prec::F16X3:
       // split A relies on one (kh, kw) cell per 32-k step (byte-identical to fp32 addressing)
-      if (d.a_split && d.conv && d.Cin < 32) throw std::invalid_argument("split activations need Cin >= 32");
+      if (d.a_split && d.conv && (d.Cin < 32 || d.KH * d.KW > 31))
+        throw std::invalid_argument("split activations need Cin >= 32 and <= 31 filter taps");
       if (d.a_split)
         launch<kF16X3S>(d, p, s);
       else

@@ -335,7 +335,7 @@ void Model::build_resnet(const PMap& p) {
   for (auto& b : blocks_) {
     const ConvW* cs[] = {&b.c1, &b.c2, &b.c3, &b.ds};
     for (const ConvW* c : cs)
-      if (c->cout && (c->cin_pad < 32 || c->cout % 32 != 0)) split_ = false;
+      if (c->cout && (c->cin_pad < 32 || c->cout % 32 != 0 || c->kh * c->kw > 31)) split_ = false;
   }
 }
 
