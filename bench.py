@@ -223,17 +223,22 @@ def measured_traffic(model, batch, precision, op):
     return ops[op]["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
 
 
-def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4):
+def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4, req_batch=None, coalesce=1,
+                delay_us=0):
     """Closed loop through the mini-runtime (host buffers, pinned slots, H2D/D2H):
-    inf/s = inferences / (last response - first request) (inference_client.cpp:259-270)."""
+    inf/s = inferences / (last response - first request) (inference_client.cpp:259-270).
+    req_batch < batch: requests of req_batch samples, merged by the runtime's dynamic
+    batching into codelet calls of up to `batch` (coalesce jobs, delay_us wait)."""
     rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
-    host_inputs, out_shape = make_inputs(name, batch, np.random.default_rng(7))
+    rb = req_batch or batch
+    host_inputs, out_shape = make_inputs(name, rb, np.random.default_rng(7))
     if name.startswith("bert"):
         in_specs = [((x.shape[1],), np.int64) for x in host_inputs]
     else:
         in_specs = [((3, 224, 224), np.float32)]
     out_elems = int(np.prod(out_shape[1:]))
-    rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers)
+    rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers,
+                       coalesce_max_jobs=coalesce, coalesce_delay_us=delay_us)
     outs = [np.empty(out_shape, np.float32) for _ in range(inflight)]
     submitted = 0
     t0 = time.perf_counter()
@@ -248,10 +253,13 @@ def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4):
     last = max(c.complete_ns for c in rt.completions)
     lat = [c.latency_ms for c in rt.completions]
     ok, failed = rt.stats()
+    jobs_per_call = float(np.mean([c.task_jobs for c in rt.completions]))
     rt.close()
-    return {"value": round(requests * batch / ((last - first) * 1e-9), 2), "unit": "inferences/s",
+    return {"value": round(requests * rb / ((last - first) * 1e-9), 2), "unit": "inferences/s",
             "p50_latency_ms": round(percentile(lat, 50), 4), "p95_latency_ms": round(percentile(lat, 95), 4),
-            "requests": requests, "batch": batch, "inflight": inflight, "workers": workers, "failed": failed,
+            "requests": requests, "request_batch": rb, "max_batch": batch, "inflight": inflight,
+            "workers": workers, "coalesce_max_jobs": coalesce, "coalesce_delay_us": delay_us,
+            "mean_jobs_per_codelet_call": round(jobs_per_call, 2), "failed": failed,
             "wall_s": round(time.perf_counter() - t0, 3)}
 
 
@@ -344,18 +352,31 @@ def main():
         from oracle.cpu_codelet import cpu_inference
 
         cores = torch.get_num_threads()
-        n, t_cpu = 0, 0.0
-        cpu_inference(model, h.host_inputs)  # warm-up
-        while t_cpu < args.cpu_seconds and n < 200:
-            ts = time.perf_counter()
-            cpu_inference(model, h.host_inputs)
-            t_cpu += time.perf_counter() - ts
-            n += 1
+
+        def cpu_sample(inputs, seconds, cap):
+            cpu_inference(model, inputs)  # warm-up
+            times = []
+            while sum(times) < seconds and len(times) < cap:
+                ts = time.perf_counter()
+                cpu_inference(model, inputs)
+                times.append(time.perf_counter() - ts)
+            return times
+
+        times = cpu_sample(h.host_inputs, args.cpu_seconds, 200)
+        t_cpu = sum(times)
         result["cpu_baseline"] = {
-            "value": round(n * args.batch / t_cpu, 3), "unit": "inferences/s", "cores": cores, "kind": "port",
-            "sample": f"{n} forwards of the same {args.model} batch {args.batch} fp32 on host ATen "
+            "value": round(len(times) * args.batch / t_cpu, 3), "unit": "inferences/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{len(times)} forwards of the same {args.model} batch {args.batch} fp32 on host ATen "
                       f"(torch {torch.__version__}, {cores} intra-op threads), {t_cpu:.1f}s",
-            "p50_ms": round(t_cpu / n * 1e3, 3)}
+            "p50_ms": round(percentile([t * 1e3 for t in times], 50), 3)}
+        if args.model == "resnet18":
+            # BASELINE configs[0] (C1): the CPU codelet alone, ResNet-18 bs=1 fp32
+            one = [x[:1] for x in h.host_inputs]
+            t1 = cpu_sample(one, min(4.0, args.cpu_seconds), 400)
+            result["cpu_baseline"]["c1_resnet18_bs1_fp32"] = {
+                "value": round(len(t1) / sum(t1), 3), "unit": "inferences/s",
+                "p50_ms": round(percentile([t * 1e3 for t in t1], 50), 3), "forwards": len(t1)}
 
     if rank == 0 and world == 1 and args.extras and args.model == "resnet18":
         extras = {}
@@ -377,6 +398,10 @@ def main():
                                   "dtype": args.precision}
         # the PCIe-inclusive serving path through the mini-runtime (never `value`)
         extras["resnet18_bs8_runtime_pcie"] = runtime_e2e(spi, replica, "resnet18", args.batch)
+        # bs=1 client requests, dynamically batched by the runtime into calls of <= 8
+        extras["resnet18_bs1_requests_batched8_runtime_pcie"] = runtime_e2e(
+            spi, replica, "resnet18", args.batch, inflight=64, requests=1280, req_batch=1, coalesce=args.batch,
+            delay_us=500)
         del r16, h16, r1, h1
         # BERT-base seq128 bs8 fp16 (BASELINE configs[2])
         bmodel = zoo.build("bert_base", seed=0)

@@ -16,6 +16,14 @@
  *                 inference_task.cpp:907-935), copy to the caller's buffer,
  *                 completion callback with the latency breakdown
  *   queue full    SPI_ERR_QUEUE_FULL (RESOURCE_EXHAUSTED, docs/server_guide.md:120)
+ *   batching      (coalesce_max_jobs > 1) a worker merges queued jobs into one task
+ *                 while the samples fit max_batch: inputs concatenated along
+ *                 dim 0 into the slot (TensorBatchCompositionPolicy::
+ *                 merge_input_tensors, batch_composition_policy.cpp:153-193),
+ *                 one codelet call, outputs sliced back per job
+ *                 (slice_outputs_for_sub_job, batching_helpers.hpp:75-125;
+ *                 ResultDispatcher::propagate_completion_to_sub_jobs,
+ *                 result_dispatcher_component.cpp:678-740)
  */
 #ifndef SPI_RUNTIME_H
 #define SPI_RUNTIME_H
@@ -39,6 +47,8 @@ typedef struct spi_job_timing {
   int64_t complete_ns;       /* outputs in the caller's buffers */
   int32_t device_id;
   int32_t worker_id;
+  int32_t task_batch;        /* samples in the codelet call that ran this job */
+  int32_t task_jobs;         /* jobs merged into that call */
 } spi_job_timing;
 
 /* Called on a runtime worker thread after the job's outputs were written (or
@@ -60,6 +70,8 @@ typedef struct spi_runtime_config {
   int32_t num_outputs;
   int32_t output_types[SPI_MAX_OUTPUTS];
   int64_t output_elems[SPI_MAX_OUTPUTS];             /* per-sample element count */
+  int32_t coalesce_max_jobs;  /* <= 1: one job per codelet call; N: merge up to N queued jobs */
+  int32_t coalesce_delay_us;  /* how long a worker waits for more jobs to fill max_batch */
 } spi_runtime_config;
 
 spi_runtime* spi_runtime_create(const spi_runtime_config* config, char* err, size_t errlen);

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -80,40 +82,64 @@ void spi_runtime::run(Worker* w) {
   (void)hipSetDevice(w->device);
   spi_set_worker_context(w->worker_id, w->device, w->stream);
   const int ni = cfg.num_inputs, no = cfg.num_outputs;
+  const int max_jobs = std::max(1, cfg.coalesce_max_jobs);
   for (;;) {
-    Job job;
+    // ---- batch composition: the queue head, then queued jobs while their samples
+    // fit max_batch (TensorBatchCompositionPolicy; the per-sample shapes are fixed
+    // by the runtime config, so every pair of jobs is mergeable)
+    std::vector<Job> jobs;
+    int64_t total = 0;
     {
       std::unique_lock<std::mutex> lk(mu);
       cv_job.wait(lk, [&] { return stop || !queue.empty(); });
       if (stop && queue.empty()) break;
-      job = std::move(queue.front());
-      queue.pop_front();
+      auto take_fitting = [&] {
+        while (!queue.empty() && (int)jobs.size() < max_jobs && total + queue.front().batch <= cfg.max_batch) {
+          total += queue.front().batch;
+          jobs.push_back(std::move(queue.front()));
+          queue.pop_front();
+        }
+      };
+      take_fitting();
+      if (max_jobs > 1 && cfg.coalesce_delay_us > 0) {
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg.coalesce_delay_us);
+        while (!stop && (int)jobs.size() < max_jobs && total < cfg.max_batch && queue.empty()) {
+          if (cv_job.wait_until(lk, deadline) == std::cv_status::timeout) break;
+          take_fitting();
+        }
+        take_fitting();
+      }
+      if (!queue.empty()) cv_job.notify_one();  // leftovers belong to another worker
     }
-    spi_job_timing t{};
-    t.submit_ns = job.submit_ns;
-    t.dequeue_ns = now_ns();
-    t.device_id = w->device;
-    t.worker_id = w->worker_id;
+    const int64_t dequeue_ns = now_ns();
     int status = SPI_OK;
     std::string err;
-    // copy_job_inputs_to_slot: caller buffers -> pinned slot -> HBM (worker stream)
-    for (int i = 0; i < ni; ++i) {
-      const size_t bytes = (size_t)job.batch * in_sample_bytes[i];
-      std::memcpy(w->h_in[i], job.in[i], bytes);
-      if (hipMemcpyAsync(w->d_in[i], w->h_in[i], bytes, hipMemcpyHostToDevice, w->stream) != hipSuccess) {
+    // copy_job_inputs_to_slot: each job's samples at its offset in the pinned slot,
+    // then one H2D per input on the worker stream
+    std::vector<int64_t> offs;
+    int64_t off = 0;
+    for (const Job& j : jobs) {
+      offs.push_back(off);
+      for (int i = 0; i < ni; ++i)
+        std::memcpy(static_cast<char*>(w->h_in[i]) + off * in_sample_bytes[i], j.in[i],
+                    (size_t)j.batch * in_sample_bytes[i]);
+      off += j.batch;
+    }
+    for (int i = 0; i < ni; ++i)
+      if (hipMemcpyAsync(w->d_in[i], w->h_in[i], (size_t)total * in_sample_bytes[i], hipMemcpyHostToDevice,
+                         w->stream) != hipSuccess) {
         status = SPI_ERR_DEVICE;
         err = "H2D copy failed";
       }
-    }
     spi_codelet_args args;
     spi_args_init(&args);
     args.num_inputs = ni;
     args.num_outputs = no;
-    args.request_id = job.request_id;
-    args.batch_size = job.batch;
+    args.request_id = jobs.front().request_id;
+    args.batch_size = total;
     for (int i = 0; i < ni; ++i) {
       args.num_dims[i] = cfg.input_ndims[i] + 1;
-      args.dims[i][0] = job.batch;
+      args.dims[i][0] = total;
       for (int d = 0; d < cfg.input_ndims[i]; ++d) args.dims[i][d + 1] = cfg.input_dims[i][d];
       args.input_types[i] = cfg.input_types[i];
     }
@@ -128,21 +154,22 @@ void spi_runtime::run(Worker* w) {
     for (int i = 0; i < ni; ++i) {
       const size_t es = spi_dtype_size(cfg.input_types[i]);
       ifaces[i] = spi_vector_interface{SPI_STARPU_VECTOR_INTERFACE_ID, (uintptr_t)w->d_in[i], 0, 0,
-                                       (uint32_t)(job.batch * in_sample_bytes[i] / es), es, 0,
+                                       (uint32_t)(total * in_sample_bytes[i] / es), es, 0,
                                        (size_t)cfg.max_batch * in_sample_bytes[i]};
       buffers[i] = &ifaces[i];
     }
     for (int i = 0; i < no; ++i) {
       const size_t es = spi_dtype_size(cfg.output_types[i]);
       ifaces[ni + i] = spi_vector_interface{SPI_STARPU_VECTOR_INTERFACE_ID, (uintptr_t)w->d_out[i], 0, 0,
-                                            (uint32_t)(job.batch * out_sample_bytes[i] / es), es, 0,
+                                            (uint32_t)(total * out_sample_bytes[i] / es), es, 0,
                                             (size_t)cfg.max_batch * out_sample_bytes[i]};
       buffers[ni + i] = &ifaces[ni + i];
     }
+    int64_t cs = 0, ce = 0;
     if (status == SPI_OK) {
       spi_hip_inference_func(buffers.data(), &args);
-      t.codelet_start_ns = args.codelet_start_ns;
-      t.codelet_end_ns = args.codelet_end_ns;
+      cs = args.codelet_start_ns;
+      ce = args.codelet_end_ns;
       if (args.status != SPI_OK) {
         status = args.status;
         err = args.error;
@@ -150,7 +177,7 @@ void spi_runtime::run(Worker* w) {
     }
     if (status == SPI_OK) {
       for (int i = 0; i < no; ++i)
-        if (hipMemcpyAsync(w->h_out[i], w->d_out[i], (size_t)job.batch * out_sample_bytes[i], hipMemcpyDeviceToHost,
+        if (hipMemcpyAsync(w->h_out[i], w->d_out[i], (size_t)total * out_sample_bytes[i], hipMemcpyDeviceToHost,
                            w->stream) != hipSuccess) {
           status = SPI_ERR_DEVICE;
           err = "D2H copy failed";
@@ -160,14 +187,31 @@ void spi_runtime::run(Worker* w) {
       status = SPI_ERR_DEVICE;
       err = "stream synchronisation failed";
     }
-    if (status == SPI_OK)
-      for (int i = 0; i < no; ++i) std::memcpy(job.out[i], w->h_out[i], (size_t)job.batch * out_sample_bytes[i]);
-    t.complete_ns = now_ns();
-    (status == SPI_OK ? completed : failed).fetch_add(1);
-    if (job.done) job.done(job.user, job.request_id, status, status == SPI_OK ? "" : err.c_str(), &t);
+    // output split: job k gets rows [offs[k], offs[k] + batch) of every output
+    // (slice_outputs_for_sub_job), then its own completion callback
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      const Job& j = jobs[k];
+      if (status == SPI_OK)
+        for (int i = 0; i < no; ++i)
+          std::memcpy(j.out[i], static_cast<const char*>(w->h_out[i]) + offs[k] * out_sample_bytes[i],
+                      (size_t)j.batch * out_sample_bytes[i]);
+      spi_job_timing t{};
+      t.submit_ns = j.submit_ns;
+      t.dequeue_ns = dequeue_ns;
+      t.codelet_start_ns = cs;
+      t.codelet_end_ns = ce;
+      t.device_id = w->device;
+      t.worker_id = w->worker_id;
+      t.task_batch = (int32_t)total;
+      t.task_jobs = (int32_t)jobs.size();
+      t.complete_ns = now_ns();
+      (status == SPI_OK ? completed : failed).fetch_add(1);
+      if (j.done) j.done(j.user, j.request_id, status, status == SPI_OK ? "" : err.c_str(), &t);
+    }
     {
       std::lock_guard<std::mutex> lk(mu);
-      if (--inflight == 0) cv_idle.notify_all();
+      inflight -= (int64_t)jobs.size();
+      if (inflight == 0) cv_idle.notify_all();
     }
   }
   spi_clear_worker_context();

@@ -1,6 +1,8 @@
 """Python host over include/spi_runtime.h: the mini-runtime that stands in for
 StarPU around the HIP codelet (eager queue, per-device HIP workers, pinned slot
-staging, H2D/D2H on the worker stream, completion callbacks)."""
+staging, H2D/D2H on the worker stream, completion callbacks, and optional
+dynamic batching: queued jobs merged into one codelet call, outputs sliced back
+per job)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -19,7 +21,7 @@ SPI_ERR_QUEUE_FULL = 8
 class JobTiming(C.Structure):
     _fields_ = [("submit_ns", C.c_int64), ("dequeue_ns", C.c_int64), ("codelet_start_ns", C.c_int64),
                 ("codelet_end_ns", C.c_int64), ("complete_ns", C.c_int64), ("device_id", C.c_int32),
-                ("worker_id", C.c_int32)]
+                ("worker_id", C.c_int32), ("task_batch", C.c_int32), ("task_jobs", C.c_int32)]
 
 
 DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.POINTER(JobTiming))
@@ -40,6 +42,8 @@ class RuntimeConfig(C.Structure):
         ("num_outputs", C.c_int32),
         ("output_types", C.c_int32 * N.SPI_MAX_OUTPUTS),
         ("output_elems", C.c_int64 * N.SPI_MAX_OUTPUTS),
+        ("coalesce_max_jobs", C.c_int32),
+        ("coalesce_delay_us", C.c_int32),
     ]
 
 
@@ -72,6 +76,8 @@ class Completion:
     complete_ns: int
     device_id: int
     worker_id: int
+    task_batch: int = 0
+    task_jobs: int = 0
 
     @property
     def latency_ms(self) -> float:
@@ -82,8 +88,11 @@ class Runtime:
     """Eager shared queue over `workers_per_device` HIP workers per replica."""
 
     def __init__(self, replicas: list[ModelReplica], input_specs, output_specs, max_batch: int,
-                 workers_per_device: int = 4, max_queue: int = 0):
-        """input_specs: [(per-sample shape, dtype)]; output_specs: [(per-sample elems, dtype)]."""
+                 workers_per_device: int = 4, max_queue: int = 0, coalesce_max_jobs: int = 1,
+                 coalesce_delay_us: int = 0):
+        """input_specs: [(per-sample shape, dtype)]; output_specs: [(per-sample elems, dtype)].
+        coalesce_max_jobs > 1 merges up to that many queued jobs (while their samples fit
+        max_batch) into one codelet call, waiting up to coalesce_delay_us for more."""
         cfg = RuntimeConfig()
         cfg.num_devices = len(replicas)
         for i, r in enumerate(replicas):
@@ -92,6 +101,8 @@ class Runtime:
         cfg.workers_per_device = workers_per_device
         cfg.max_batch = max_batch
         cfg.max_queue = max_queue
+        cfg.coalesce_max_jobs = coalesce_max_jobs
+        cfg.coalesce_delay_us = coalesce_delay_us
         cfg.num_inputs = len(input_specs)
         self._in_dtypes = []
         for i, (shape, dt) in enumerate(input_specs):
@@ -117,7 +128,8 @@ class Runtime:
     def _done(self, _user, request_id, status, error, t):
         tt = t.contents
         c = Completion(request_id, status, (error or b"").decode(), tt.submit_ns, tt.dequeue_ns,
-                       tt.codelet_start_ns, tt.codelet_end_ns, tt.complete_ns, tt.device_id, tt.worker_id)
+                       tt.codelet_start_ns, tt.codelet_end_ns, tt.complete_ns, tt.device_id, tt.worker_id,
+                       tt.task_batch, tt.task_jobs)
         with self._lock:
             self._pending.pop(request_id, None)
             self.completions.append(c)

@@ -64,7 +64,8 @@ int main(void) {
   F(spi_codelet_args, executed_on) F(spi_codelet_args, status) F(spi_codelet_args, error)
   S(spi_runtime_config) F(spi_runtime_config, models) F(spi_runtime_config, workers_per_device)
   F(spi_runtime_config, input_dims) F(spi_runtime_config, num_outputs) F(spi_runtime_config, output_elems)
-  S(spi_job_timing) F(spi_job_timing, complete_ns) F(spi_job_timing, worker_id)
+  F(spi_runtime_config, coalesce_max_jobs) F(spi_runtime_config, coalesce_delay_us)
+  S(spi_job_timing) F(spi_job_timing, complete_ns) F(spi_job_timing, worker_id) F(spi_job_timing, task_jobs)
   return 0;
 }
 """

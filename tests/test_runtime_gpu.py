@@ -82,3 +82,57 @@ def test_runtime_reports_codelet_failures_and_queue_full(spi, zoo, rtmod):
     rt.drain()
     assert rejected > 0 and rt.stats()[0] == 64 - rejected
     rt.close()
+
+
+def test_runtime_dynamic_batching_merges_and_slices(spi, zoo, rtmod):
+    """Queued jobs of ragged sizes merged into one codelet call (merge_input_tensors,
+    batch_composition_policy.cpp:153-193) and the outputs sliced back per job
+    (slice_outputs_for_sub_job, batching_helpers.hpp:75-125): every job's rows equal
+    its own forward."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp32", max_batch=8, image_size=64)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8,
+                       workers_per_device=1, coalesce_max_jobs=8, coalesce_delay_us=200_000)
+    rng = np.random.default_rng(3)
+    sizes = [1, 3, 2, 1, 1, 4, 2, 1, 3, 1]
+    jobs = []
+    for rid, b in enumerate(sizes):
+        x = rng.random((b, 3, 64, 64), dtype=np.float32)
+        y = np.full((b, 1000), np.nan, dtype=np.float32)
+        rt.submit(rid, [x], [y])
+        jobs.append((x, y))
+    rt.drain()
+    assert rt.stats() == (len(sizes), 0)
+    for x, y in jobs:
+        assert normalized_max_error(y, cpu_inference(m, [x])[0]) < 1e-5
+    by_id = {c.request_id: c for c in rt.completions}
+    assert max(c.task_jobs for c in rt.completions) > 1  # something was merged
+    for c in rt.completions:
+        assert 1 <= c.task_jobs <= 8 and c.task_batch <= 8
+        assert c.submit_ns <= c.dequeue_ns <= c.codelet_start_ns <= c.codelet_end_ns <= c.complete_ns
+    # jobs merged into one call share its codelet stamps and batch
+    groups = {}
+    for rid, c in by_id.items():
+        groups.setdefault((c.codelet_start_ns, c.worker_id), []).append(sizes[rid])
+    for (start, _), members in groups.items():
+        assert sum(members) == next(c.task_batch for c in rt.completions if c.codelet_start_ns == start)
+    rt.close()
+
+
+def test_runtime_bs1_requests_batched_to_8(spi, zoo, rtmod):
+    """The serving shape of the reference's client: bs=1 requests, batched server-side."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=8, image_size=64)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8,
+                       workers_per_device=2, coalesce_max_jobs=8, coalesce_delay_us=50_000)
+    rng = np.random.default_rng(4)
+    xs = [rng.random((1, 3, 64, 64), dtype=np.float32) for _ in range(32)]
+    ys = [np.zeros((1, 1000), np.float32) for _ in range(32)]
+    for i in range(32):
+        rt.submit(i, [xs[i]], [ys[i]])
+    rt.drain()
+    assert rt.stats() == (32, 0)
+    ref = cpu_inference(m, [np.concatenate(xs)])[0]
+    assert normalized_max_error(np.concatenate(ys), ref) < 1e-5
+    assert sum(c.task_jobs for c in rt.completions) / len(rt.completions) > 1.5
+    rt.close()
