@@ -7,6 +7,13 @@
  * pointers are device pointers unless marked host; every call only enqueues
  * on `stream`.  Return 0 on success, non-zero on invalid arguments / HIP error
  * (message in spi_last_error()).
+ *
+ * precision: 0 fp32, 1 fp16, 2 fp16x3 (fp32 activations split into hi/lo fp16
+ * at fragment read), 3 fp16x3 on SPLIT activations: every activation operand
+ * (A, residual, C) uses the split layout the fp16x3 ResNet forward keeps in
+ * HBM -- per row, blocks of 32 elements stored as [32 hi fp16 | 32 lo fp16]
+ * (128 bytes, the size of 32 fp32), hi = fp16(x), lo = fp16(x - hi).  It needs
+ * K (GEMM) / Cin (conv) and N / Cout to be multiples of 32 and <= 31 filter taps.
  */
 #ifndef SPI_OPS_H
 #define SPI_OPS_H
@@ -19,8 +26,8 @@ extern "C" {
 #endif
 
 /* Packed weight layout for a [N][K] fp32 matrix: rows padded to Npad = 128k,
- * columns to Kpad = 64k; fp16 / fp32 elements, or for fp16x3 per 32-k block
- * [32 hi fp16 | 32 lo fp16].  Returns the packed byte count; writes Npad/Kpad. */
+ * columns to Kpad = 64k; fp16 / fp32 elements, or for fp16x3 (2 and 3) per
+ * 32-k block [32 hi fp16 | 32 lo fp16].  Returns the packed byte count; writes Npad/Kpad. */
 size_t spi_op_packed_bytes(int32_t precision, int32_t N, int32_t K, int32_t* Npad, int32_t* Kpad);
 /* Host-side packing: w_host fp32 [N][K] -> dst_host (spi_op_packed_bytes bytes). */
 int spi_op_pack_weight(int32_t precision, const float* w_host, int32_t N, int32_t K, void* dst_host);
@@ -30,15 +37,17 @@ int spi_op_pack_weight(int32_t precision, const float* w_host, int32_t N, int32_
 size_t spi_op_workspace_bytes(void);
 
 /* C[M,N] = act(A[M,K] . W^T + bias + residual); act: 0 none, 1 relu, 2 gelu.
- * A: fp16 (precision fp16) or fp32 (fp32 / fp16x3), row stride lda.
- * residual: same element type as A unless res_f32; C: fp32 when out_f32. */
+ * A: fp16 (precision fp16), fp32 (fp32 / fp16x3) or split (3), row stride lda
+ * (elements).  residual: same element type as A unless res_f32; C: fp32 when
+ * out_f32 (not with split). */
 int spi_op_gemm(int32_t precision, const void* A, int32_t M, int32_t K, int32_t lda,
                 const void* W_packed, int32_t N, const float* bias, const void* residual,
                 int32_t res_f32, int32_t ldr, void* C, int32_t out_f32, int32_t ldc,
                 int32_t act, void* workspace, void* stream);
 
 /* NHWC conv as implicit GEMM: x [B][H][W][Cin] (Cin a power of two >= 8 for fp16,
- * >= 4 for fp32 / fp16x3), W packed from [Cout][KH][KW][Cin] order, y [B][OH][OW][Cout]. */
+ * >= 4 for fp32 / fp16x3, >= 32 for split), W packed from [Cout][KH][KW][Cin]
+ * order, y [B][OH][OW][Cout]; residual (optional) shaped like y. */
 int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_t W,
                   int32_t Cin, const void* W_packed, int32_t Cout, int32_t KH, int32_t KW,
                   int32_t stride, int32_t pad, const float* bias, const void* residual,

@@ -20,10 +20,12 @@ constexpr size_t kSlabFloats = (size_t)8 << 20;  // 32 MiB of split-K slabs
 bool prec_of(int32_t p, spi::Prec* out) {
   if (p == 0) *out = spi::Prec::F32;
   else if (p == 1) *out = spi::Prec::F16;
-  else if (p == 2) *out = spi::Prec::F16X3;
+  else if (p == 2 || p == 3) *out = spi::Prec::F16X3;  // 3: split activations
   else return false;
   return true;
 }
+
+constexpr int32_t kSplitPrecision = 3;
 
 int fail(const std::string& m) {
   spi_set_last_error(m.c_str());
@@ -86,6 +88,11 @@ int spi_op_gemm(int32_t precision, const void* A, int32_t M, int32_t K, int32_t 
   d.act = static_cast<spi::Act>(act);
   d.out_f32 = out_f32 != 0;
   d.res_f32 = res_f32 != 0;
+  if (precision == kSplitPrecision) {
+    if (K % 32 || N % 32 || lda % 32 || ldc % 32 || out_f32 || res_f32 || (residual && ldr % 32))
+      return fail("split gemm needs K, N and strides multiples of 32, no fp32 operands");
+    d.a_split = d.out_split = true;
+  }
   if (spi::gemm_partial_floats(d, p) > kSlabFloats || spi::gemm_counter_slots(d, p) > kTickets)
     return fail("gemm too large for the op workspace");
   spi::GemmPtrs ptrs = scratch(workspace);
@@ -125,6 +132,11 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
   d.ldc = Cout;
   d.ldr = Cout;
   d.act = static_cast<spi::Act>(act);
+  if (precision == kSplitPrecision) {
+    if (Cin < 32 || Cout % 32 || KH * KW > 31)
+      return fail("split conv needs Cin >= 32, Cout a multiple of 32 and <= 31 filter taps");
+    d.a_split = d.out_split = true;
+  }
   if (spi::gemm_partial_floats(d, p) > kSlabFloats || spi::gemm_counter_slots(d, p) > kTickets)
     return fail("conv too large for the op workspace");
   spi::GemmPtrs ptrs = scratch(workspace);
@@ -147,7 +159,8 @@ int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias,
 
 int spi_op_layernorm(int32_t precision, const float* x, const float* g, const float* b, float* yf, void* yt,
                      int32_t rows, int32_t D, float eps, void* stream) {
-  if (!x || !g || !b || rows <= 0 || D <= 0 || D > 1024 || (!yf && !yt)) return fail("invalid layernorm arguments");
+  if (precision < 0 || precision > 2 || !x || !g || !b || rows <= 0 || D <= 0 || D > 1024 || (!yf && !yt))
+    return fail("invalid layernorm arguments");
   spi::layernorm(x, D, g, b, yf, yt, D, rows, D, eps, precision == 1, static_cast<hipStream_t>(stream));
   return check_launch();
 }

@@ -13,7 +13,7 @@ import torch
 from . import _native as N
 from ._native import lib
 
-PREC = {"fp32": 0, "fp16": 1, "fp16x3": 2}
+PREC = {"fp32": 0, "fp16": 1, "fp16x3": 2, "fp16x3s": 3}  # fp16x3s: split activation layout
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
 
 
@@ -32,6 +32,24 @@ def _check(rc):
 
 def act_dtype(prec: str) -> torch.dtype:
     return torch.float16 if prec == "fp16" else torch.float32
+
+
+def to_split(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [..., C] (C % 32 == 0) -> the split layout (fp16x3s operands), stored in a
+    float32 tensor of the same shape: per 32-channel block [32 hi fp16 | 32 lo fp16]."""
+    x = x.float().contiguous()
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    blk = x.shape[-1] // 32
+    s = torch.cat([hi.reshape(*x.shape[:-1], blk, 32), lo.reshape(*x.shape[:-1], blk, 32)], dim=-1)
+    return s.contiguous().view(torch.float32).reshape(x.shape)
+
+
+def from_split(s: torch.Tensor) -> torch.Tensor:
+    """Inverse of to_split: hi + lo in fp32."""
+    blk = s.shape[-1] // 32
+    h = s.contiguous().view(torch.float16).reshape(*s.shape[:-1], blk, 64)
+    return (h[..., :32].float() + h[..., 32:].float()).reshape(s.shape)
 
 
 def pack_weight(prec: str, w: np.ndarray | torch.Tensor, device="cuda") -> torch.Tensor:
@@ -62,13 +80,14 @@ def gemm(prec, A, W_packed, N_, bias=None, residual=None, out=None, out_f32=True
     M, K = A.shape
     if out is None:
         out = torch.empty(M, N_, device=A.device, dtype=torch.float32 if out_f32 else act_dtype(prec))
+    split = prec == "fp16x3s"  # float32-storage tensors holding the split layout, not fp32 values
     if res_f32 is None:
-        res_f32 = residual is not None and residual.dtype == torch.float32
+        res_f32 = residual is not None and residual.dtype == torch.float32 and not split
     ws = workspace(A.device) if ws is None else ws
     s = torch.cuda.current_stream().cuda_stream if stream is None else stream
     _check(lib.spi_op_gemm(PREC[prec], _ptr(A), M, K, A.stride(0), _ptr(W_packed), N_, _ptr(bias), _ptr(residual),
                            int(res_f32), residual.stride(0) if residual is not None else 0, _ptr(out),
-                           int(out.dtype == torch.float32), out.stride(0), ACT[act], _ptr(ws), C.c_void_p(s)))
+                           int(out.dtype == torch.float32 and not split), out.stride(0), ACT[act], _ptr(ws), C.c_void_p(s)))
     return out
 
 

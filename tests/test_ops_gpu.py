@@ -122,3 +122,53 @@ def test_layernorm(ops, prec, rows, D, eps):
     assert normalized_max_error(yf.cpu().numpy(), ref.numpy()) < 2e-6
     if prec == "fp16":
         assert normalized_max_error(yt.float().cpu().numpy(), ref.numpy()) < 1e-3
+
+
+# ---- fp16x3 on split activations (precision 3, the layout the fp16x3 ResNet forward keeps in HBM) ----
+
+@pytest.mark.parametrize("B,H,cin,cout,k,stride,res", [(3, 56, 64, 64, 3, 1, True), (2, 56, 64, 128, 3, 2, False),
+                                                       (2, 28, 128, 128, 3, 1, True), (2, 14, 256, 512, 1, 2, False),
+                                                       (4, 7, 512, 512, 3, 1, True), (1, 9, 32, 96, 3, 1, True)])
+def test_conv2d_split_layout(ops, B, H, cin, cout, k, stride, res):
+    """Split A / residual / output conv (the tap-walk kernel of every fp16x3 ResNet conv
+    but the stem) vs an fp32 conv on the values the split layout holds."""
+    g = torch.Generator().manual_seed(B * 100 + H + cin + cout + k)
+    x = torch.randn(B, H, H, cin, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g)
+    pad = k // 2
+    oh = (H + 2 * pad - k) // stride + 1
+    r = torch.randn(B, oh, oh, cout, generator=g) if res else None
+    xs = ops.to_split(x)
+    x_val = ops.from_split(xs)  # the values the kernel sees (hi + lo)
+    ref = F.conv2d(x_val.permute(0, 3, 1, 2), w, b, stride, pad).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + ops.from_split(ops.to_split(r))
+    ref = F.relu(ref)
+    wp = ops.pack_weight("fp16x3s", ops.conv_weight_matrix(w, cin))
+    out = ops.conv2d("fp16x3s", xs.cuda(), wp, cout, k, k, stride, pad, bias=b.cuda(), act="relu",
+                     residual=ops.to_split(r).cuda() if res else None)
+    err = normalized_max_error(ops.from_split(out.cpu()).numpy(), ref.numpy())
+    assert err < 1e-5, f"split conv {B}x{H}x{cin}->{cout} k{k}s{stride}: {err:.3e}"
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (100, 96, 160), (392, 512, 4608), (1024, 768, 3072)])
+def test_gemm_split_layout(ops, M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    As, Rs = ops.to_split(A), ops.to_split(R)
+    ref = ops.from_split(As) @ W.T + b + ops.from_split(Rs)
+    out = ops.gemm("fp16x3s", As.cuda(), ops.pack_weight("fp16x3s", W), N, bias=b.cuda(), residual=Rs.cuda(),
+                   out=torch.empty(M, N, device="cuda"))
+    err = normalized_max_error(ops.from_split(out.cpu()).numpy(), ref.numpy())
+    assert err < 1e-5, f"split gemm {M}x{N}x{K}: {err:.3e}"
+
+
+def test_split_layout_rejects_bad_shapes(ops):
+    x = torch.zeros(1, 8, 8, 16, device="cuda")
+    wp = ops.pack_weight("fp16x3s", np.zeros((32, 9 * 16), np.float32))
+    with pytest.raises(ops.OpError):
+        ops.conv2d("fp16x3s", x, wp, 32, 3, 3, 1, 1)  # Cin 16 < 32
