@@ -59,6 +59,20 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
   } while (0)
 #endif
 
+// Diagnostic builds: -DSPI_DIAG_NO_DMA issues no LDS-DMA (the tiles hold stale
+// bytes), -DSPI_DIAG_NO_MFMA reads the fragments but issues no MFMA; timed
+// against the real kernel (tools/ab_gemm.py) they split a launch into data
+// movement and matrix work.  Outputs of both are meaningless.
+#ifdef SPI_DIAG_NO_DMA
+#define SPI_DMA(src, dst, sz, off, aux) \
+  do {                                  \
+    (void)(src);                        \
+    (void)(dst);                        \
+  } while (0)
+#else
+#define SPI_DMA(src, dst, sz, off, aux) __builtin_amdgcn_global_load_lds(src, dst, sz, off, aux)
+#endif
+
 struct KArgs {
   GemmDesc d;
   GemmPtrs p;
@@ -68,6 +82,7 @@ struct KArgs {
   int cin_shift;
   int kw_mul;       // ceil(65536 / KW): cell / KW == (cell * kw_mul) >> 16 for cell < 2^12
   int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
+  int vec_ok;       // C / residual rows allow 16-byte vectors of 8 elements (epilogue)
 };
 
 template <int MODE>
@@ -285,7 +300,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
         for (int q = 0; q < AQ; ++q) {
           const bool ok = (a_mask[q] >> cu_cell) & 1u;
           const char* src = ok ? reinterpret_cast<const char*>(a_src[q] + cu_off) : zeros;
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
         // advance one k-step: next channel block, or the next tap (next pixel,
         // or the next filter row: W - KW + 1 pixels on)
@@ -313,7 +328,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
             if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W)
               src = reinterpret_cast<const char*>(a_base[q] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c);
           }
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
       }
     } else {
@@ -321,13 +336,13 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       for (int q = 0; q < AQ; ++q) {
         const int k = k0 + a_koff[q];
         const char* src = (a_ok[q] && k < d.K) ? reinterpret_cast<const char*>(a_pix[q] + k) : zeros;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+        SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
     // k-step byte offset inside a W row: RB bytes per step (advanced per issue).
 #pragma unroll
     for (int q = 0; q < BQ; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[q] + w_kb),
+      SPI_DMA((const void*)(b_src[q] + w_kb),
                                        (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
     w_kb += RB;
   };
@@ -342,54 +357,58 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // Bias fetched up front (TJ floats; out-of-tile lanes read the zero line).
-  // The residual is NOT prefetched into registers: holding it across the K
-  // loop cost 30-70 VGPRs and a wave per SIMD, which lost 15 % end to end
-  // (34.7k vs 40.9k inf/s, ResNet-18 fp16x3, 4 workers); the epilogue batches
-  // its residual loads once the loop registers are dead instead.
-  float bpre[TJ];
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int n = n0 + wn * WTN + j * 16 + fr;
-    bpre[j] = (a.p.bias ? a.p.bias : reinterpret_cast<const float*>(zeros))[a.p.bias && n < d.N ? n : 0];
-  }
-
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) issue(s, s);
 
-  // Epilogue, one fragment row-group (i) at a time to bound registers, each in
-  // three branch-free phases (per-element runtime branches made the waitcnt
-  // pass fall back to vmcnt(0) after every store): the group's residual loads
-  // (clamped, always-valid addresses), then bias + residual + activation in
-  // registers (activation chosen once), then the stores (one loop per output
-  // format).
+  // Epilogue through LDS (the K loop's ring is free by then; cdna_hip_programming.md
+  // T21, store-issue-bound tails).  The waves park their raw accumulators as an fp32
+  // [BM][BN] tile -- 16-column blocks XOR-swizzled by (row >> 2) & 3, so the
+  // ds_write_b32 of a fragment (4 row groups x 16 columns) hits 64 distinct banks --
+  // then every thread owns one 8-column group and walks rows, moving bias, residual
+  // and output as 16-byte vectors (global_load/store_dwordx4) instead of the 2-4 byte
+  // per-element accesses of the fragment layout (a 128x64 split tile: 16 vector
+  // accesses per thread instead of 128 scalar ones).  All residual loads of a thread
+  // go out before its first store (clamped rows: always-valid addresses, no branch).
+  // Tiles crossing N, or unaligned strides, take the per-element path from LDS.
   auto finish = [&](floatx4 (&v)[TI][TJ]) {
     using Out = typename TR::Out;
-    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : d.out_f32 ? 1 : 0;
+    static_assert(BM * BN * 4 <= STAGES * IMG, "the C tile must fit the LDS ring");
+    float* T = reinterpret_cast<float*>(lds);
+    __syncthreads();  // every wave is done reading the ring
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      float x[TJ][4];
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[j][r] = 0.f;
-      if (a.p.res) {
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + fq * 4 + r;
+          const int col = (wn * WTN + j * 16 + fr) ^ (fq << 4);  // (row >> 2) & 3 == fq
+          T[row * BN + col] = v[i][j][r];
+        }
+    __syncthreads();
+    constexpr int G = BN / 8, RSTEP = 256 / G, ITEMS = BM / RSTEP;
+    const int cg = tid % G, r0 = tid / G;
+    const int nb = n0 + cg * 8;
+    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
+    auto tile_vals = [&](int row, float (&y)[8]) {
+      const float* src = T + row * BN + ((cg * 8) ^ (((row >> 2) & 3) << 4));
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-            const int n = n0 + wn * WTN + j * 16 + fr;
-            x[j][r] = load_res<MODE>(a, m < d.M ? m : 0, n < d.N ? n : 0);
-          }
+      for (int e = 0; e < 4; ++e) {
+        y[e] = x0[e];
+        y[e + 4] = x1[e];
       }
+    };
+    auto finish_act = [&](auto& y) {
+      constexpr int NI = sizeof(y) / sizeof(y[0]);
       auto apply = [&](auto act_tag) {
         constexpr Act act = decltype(act_tag)::value;
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
+        for (int it = 0; it < NI; ++it)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) x[j][r] = apply_act(v[i][j][r] + bpre[j] + x[j][r], act);
+          for (int e = 0; e < 8; ++e) y[it][e] = apply_act(y[it][e], act);
       };
       if (d.act == Act::Relu)
         apply(std::integral_constant<Act, Act::Relu>{});
@@ -397,30 +416,112 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
         apply(std::integral_constant<Act, Act::Gelu>{});
       else
         apply(std::integral_constant<Act, Act::None>{});
-      auto store_all = [&](auto st) {
+    };
+    float b[8];
+    if (a.vec_ok && n0 + BN <= d.N) {
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
+      for (int e = 0; e < 8; ++e) b[e] = a.p.bias ? a.p.bias[nb + e] : 0.f;
+      // rows in chunks of <= 4 per thread: the residual loads of a chunk are all in
+      // flight before its first store, within a bounded register budget
+      constexpr int CH = ITEMS < 4 ? ITEMS : 4;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-            const int n = n0 + wn * WTN + j * 16 + fr;
-            if (m < d.M && n < d.N) st(m, n, x[j][r]);
+      for (int c0 = 0; c0 < ITEMS; c0 += CH) {
+        float y[CH][8];
+#pragma unroll
+        for (int it = 0; it < CH; ++it) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[it][e] = 0.f;
+        }
+        if (a.p.res) {
+#pragma unroll
+          for (int it = 0; it < CH; ++it) {
+            const int m = min(m0 + r0 + (c0 + it) * RSTEP, d.M - 1);
+            if constexpr (MODE == kF16X3S) {
+              const _Float16* R = static_cast<const _Float16*>(a.p.res) + split_idx(m, nb, d.ldr);
+              const half8 hi = *reinterpret_cast<const half8*>(R);
+              const half8 lo = *reinterpret_cast<const half8*>(R + 32);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
+            } else if (d.res_f32 || sizeof(Out) == 4) {
+              const float* R = static_cast<const float*>(a.p.res) + (size_t)m * d.ldr + nb;
+              const floatx4 r0v = *reinterpret_cast<const floatx4*>(R);
+              const floatx4 r1v = *reinterpret_cast<const floatx4*>(R + 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                y[it][e] = r0v[e];
+                y[it][e + 4] = r1v[e];
+              }
+            } else {
+              const half8 r = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(a.p.res) +
+                                                              (size_t)m * d.ldr + nb);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(r[e]);
+            }
           }
-      };
-      if (fmt == 2) {
-        _Float16* C = static_cast<_Float16*>(a.p.C);
-        store_all([&](int m, int n, float y) {
+        }
+#pragma unroll
+        for (int it = 0; it < CH; ++it) {
+          float t[8];
+          tile_vals(r0 + (c0 + it) * RSTEP, t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[it][e] = t[e] + b[e] + y[it][e];  // acc + bias + residual
+        }
+        finish_act(y);
+#pragma unroll
+        for (int it = 0; it < CH; ++it) {
+          const int m = m0 + r0 + (c0 + it) * RSTEP;
+          if (m >= d.M) continue;
+          if (fmt == 2) {
+            half8 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              hi[e] = static_cast<_Float16>(y[it][e]);
+              lo[e] = static_cast<_Float16>(y[it][e] - static_cast<float>(hi[e]));
+            }
+            _Float16* C = static_cast<_Float16*>(a.p.C) + split_idx(m, nb, d.ldc);
+            *reinterpret_cast<half8*>(C) = hi;
+            *reinterpret_cast<half8*>(C + 32) = lo;
+          } else if (fmt == 1) {
+            float* C = static_cast<float*>(a.p.C) + (size_t)m * d.ldc + nb;
+            *reinterpret_cast<floatx4*>(C) = floatx4{y[it][0], y[it][1], y[it][2], y[it][3]};
+            *reinterpret_cast<floatx4*>(C + 4) = floatx4{y[it][4], y[it][5], y[it][6], y[it][7]};
+          } else {
+            half8 h;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(y[it][e]);
+            *reinterpret_cast<half8*>(static_cast<_Float16*>(a.p.C) + (size_t)m * d.ldc + nb) = h;
+          }
+        }
+      }
+      return;
+    }
+    // per-element path (tiles crossing N, unaligned strides)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (a.p.bias && nb + e < d.N) ? a.p.bias[nb + e] : 0.f;
+    for (int it = 0; it < ITEMS; ++it) {
+      const int row = r0 + it * RSTEP, m = m0 + row;
+      if (m >= d.M) continue;
+      float y[8];
+      tile_vals(row, y);
+      for (int e = 0; e < 8; ++e) {
+        const float r = (a.p.res && nb + e < d.N) ? load_res<MODE>(a, m, nb + e) : 0.f;
+        y[e] = apply_act(y[e] + b[e] + r, d.act);
+      }
+      for (int e = 0; e < 8; ++e) {
+        const int n = nb + e;
+        if (n >= d.N) break;
+        const float val = y[e];
+        if (fmt == 2) {
+          _Float16* C = static_cast<_Float16*>(a.p.C);
           const size_t k = split_idx(m, n, d.ldc);
-          const _Float16 hi = static_cast<_Float16>(y);
+          const _Float16 hi = static_cast<_Float16>(val);
           C[k] = hi;
-          C[k + 32] = static_cast<_Float16>(y - static_cast<float>(hi));
-        });
-      } else if (fmt == 1) {
-        float* C = static_cast<float*>(a.p.C);
-        store_all([&](int m, int n, float y) { C[(size_t)m * d.ldc + n] = y; });
-      } else {
-        Out* C = static_cast<Out*>(a.p.C);
-        store_all([&](int m, int n, float y) { C[(size_t)m * d.ldc + n] = static_cast<Out>(y); });
+          C[k + 32] = static_cast<_Float16>(val - static_cast<float>(hi));
+        } else if (fmt == 1) {
+          static_cast<float*>(a.p.C)[(size_t)m * d.ldc + n] = val;
+        } else {
+          static_cast<_Float16*>(a.p.C)[(size_t)m * d.ldc + n] = static_cast<_Float16>(val);
+        }
       }
     }
   };
@@ -476,7 +577,11 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
+#ifdef SPI_DIAG_NO_MFMA  // diagnostic build: fragments read, no matrix work
+            asm volatile("" ::"v"(af[kk][i]), "v"(bf[kk][j]));
+#else
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
+#endif
     } else if constexpr (kSplitMode<MODE>) {
       static_assert(ESTEP == 32, "one 32-k block per step");
       // fp32 A: two 16-byte chunks split into hi/lo below; split A: hi and lo
@@ -511,9 +616,13 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
+#ifdef SPI_DIAG_NO_MFMA
+          asm volatile("" ::"v"(al[i]), "v"(ah[i]), "v"(bh[j]), "v"(bl[j]));
+#else
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#endif
         }
     } else {
       floatx4 a0[TI], a1[TI], b0[TJ], b1[TJ];
@@ -781,6 +890,8 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
   // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
   a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP && d.KH * d.KW <= 31;
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  a.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res)));
   const dim3 grid(a.tiles, pl.splits);
   if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(a, grid, s);

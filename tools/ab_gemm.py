@@ -9,12 +9,13 @@ second conv of each basic block with its residual), i.e. the headline's kernels.
 """
 import argparse
 import ctypes as C
+import os
 
 import numpy as np
 import torch
 
 V = C.c_void_p
-PREC = {"fp32": 0, "fp16": 1, "fp16x3": 2}
+PREC = {"fp32": 0, "fp16": 1, "fp16x3": 2, "fp16x3s": 3}  # fp16x3s: split activation layout
 # (B, H, Cin, Cout, k, stride, residual)
 RESNET18 = [(8, 224, 8, 64, 7, 2, False), (8, 56, 64, 64, 3, 1, False), (8, 56, 64, 64, 3, 1, True),
             (8, 56, 64, 128, 3, 2, False), (8, 28, 128, 128, 3, 1, True), (8, 56, 64, 128, 1, 2, False),
@@ -63,22 +64,48 @@ def main():
     ap.add_argument("libs", nargs=2)
     ap.add_argument("--prec", default="fp16,fp16x3")
     ap.add_argument("--set", default="all", choices=["resnet18", "gemm", "all"])
+    ap.add_argument("--env-a", default="", help="knobs for lib A only, e.g. 'SPI_GEMM_NG=2' (comma-separated)")
+    ap.add_argument("--env-b", default="", help="knobs for lib B only")
     a = ap.parse_args()
+    if a.libs[0] == a.libs[1]:  # same file twice: load a private copy so each keeps its own knobs
+        import shutil
+        import tempfile
+        cp = os.path.join(tempfile.mkdtemp(), "libspi_b.so")
+        shutil.copy(a.libs[1], cp)
+        a.libs[1] = cp
     libs = [load(p) for p in a.libs]
+    for lib, spec in zip(libs, [a.env_a, a.env_b]):  # knobs are cached per library: set, reload, restore
+        kv = [s.split("=", 1) for s in spec.split(",") if s]
+        old = {k: os.environ.get(k) for k, _ in kv}
+        os.environ.update(dict(kv))
+        lib.spi_debug_gemm_reload_env()
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     ws = [torch.zeros(l.spi_op_workspace_bytes(), dtype=torch.uint8, device="cuda") for l in libs]
     s = torch.cuda.current_stream().cuda_stream
     for pname in a.prec.split(","):
         prec = PREC[pname]
         dt = torch.float16 if pname == "fp16" else torch.float32
+        split = pname == "fp16x3s"  # split layout: [.., C] as 2C fp16 (hi | lo per 32-block)
+
+        def act(*shape):
+            if split:
+                return torch.randn(*shape[:-1], 2 * shape[-1], device="cuda").half()
+            return torch.randn(*shape, device="cuda").to(dt)
         tot = [0.0, 0.0]
         if a.set in ("resnet18", "all"):
             for (B, H, cin, cout, k, st, has_res) in RESNET18:
-                x = torch.randn(B, H, H, cin, device="cuda").to(dt)
+                if split and cin < 32:
+                    continue
+                x = act(B, H, H, cin)
                 wp = packed(libs[0], prec, cout, k * k * cin)
                 bias = torch.randn(cout, device="cuda")
                 oh = (H + 2 * (k // 2) - k) // st + 1
-                res = torch.randn(B, oh, oh, cout, device="cuda").to(dt) if has_res else None
-                ys = [torch.empty(B, oh, oh, cout, device="cuda", dtype=dt) for _ in libs]
+                res = act(B, oh, oh, cout) if has_res else None
+                ys = [torch.empty_like(act(B, oh, oh, cout)) for _ in libs]
                 fns = [(lambda l=l, y=y, w=w: l.spi_op_conv2d(
                     prec, x.data_ptr(), B, H, H, cin, wp.data_ptr(), cout, k, k, st, k // 2, bias.data_ptr(),
                     res.data_ptr() if res is not None else None, y.data_ptr(), 1, w.data_ptr(), s))
@@ -93,11 +120,11 @@ def main():
             print(f"{pname:6s} resnet18 conv sum: A {tot[0]:.1f} us  B {tot[1]:.1f} us  B/A {tot[1] / tot[0]:.3f}")
         if a.set in ("gemm", "all"):
             for M, N, K in GEMMS:
-                A = torch.randn(M, K, device="cuda").to(dt)
+                A = act(M, K)
                 wp = packed(libs[0], prec, N, K)
-                outs = [torch.empty(M, N, device="cuda") for _ in libs]
+                outs = [torch.empty_like(act(M, N)) if split else torch.empty(M, N, device="cuda") for _ in libs]
                 fns = [(lambda l=l, o=o, w=w: l.spi_op_gemm(prec, A.data_ptr(), M, K, K, wp.data_ptr(), N, None, None,
-                                                           0, 0, o.data_ptr(), 1, N, 0, w.data_ptr(), s))
+                                                           0, 0, o.data_ptr(), 0 if split else 1, N, 0, w.data_ptr(), s))
                        for l, o, w in zip(libs, outs, ws)]
                 t = time_pair(fns)
                 print(f"{pname:6s} gemm {M}x{N}x{K}: A {t[0]:.2f} us ({2 * M * N * K / t[0] / 1e6:.0f} TF/s)  "
