@@ -83,6 +83,11 @@ struct KArgs {
   int kw_mul;       // ceil(65536 / KW): cell / KW == (cell * kw_mul) >> 16 for cell < 2^12
   int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
   int vec_ok;       // C / residual rows allow 16-byte vectors of 8 elements (epilogue)
+  // halo conv (kConvHalo): tiles are bands of h_th output rows x the full width of
+  // one image; h_nb bands per image; the band's input rows (+1 pixel of padding
+  // around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel blocks,
+  // h_bps of them per split-K slice
+  int h_th, h_nb, h_hwp, h_hp, h_nblk, h_bps;
 };
 
 template <int MODE>
@@ -175,32 +180,55 @@ __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
 // occupancy each tile reaches within its registers: 4 / 3 / 2 waves per SIMD.
 template <int BM, int BN>
 constexpr bool kSplitK = BM == 64 && BN == 64;
-// Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
-// size, capped by what the tile's LDS ring allows (one wave per SIMD per block,
-// 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
-template <int BM, int BN, int STAGES>
-constexpr int kMinWaves = std::min(BM * BN <= 64 * 64 ? 4 : BM * BN <= 128 * 64 ? 3 : 2,
-                                   (160 * 1024) / (STAGES * (BM + BN) * 128 + 16));
 
 // A-operand kinds: dense rows; conv with one (kh, kw) tap per k-step (Cin >= the
 // k-step: scalar tap walk + per-row tap mask); conv in general (per-chunk taps:
-// the stem).  Separate instantiations keep each kind's loop free of the others.
-enum : int { kDense = 0, kConvTap = 1, kConvGen = 2 };
+// the stem); 3x3/s1/p1 conv from an LDS-resident input band (kConvHalo, below).
+// Separate instantiations keep each kind's loop free of the others.
+enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3 };
+
+// kConvHalo.  An implicit-GEMM conv stages each (tap, channel block) A tile
+// separately: every input pixel crosses the CU nine times, and the vector-memory
+// ingest of a CU (~70 GB/s from L2, MI355X_MICROARCH.md "gather into LDS") is
+// what bounds these layers (no-DMA diagnostic build: +64 % end to end).  Here a
+// tile is a band of whole output rows of one image; per channel block the band's
+// input rows plus the 1-pixel border -- (th + 2) x (W + 2) pixels, 128 bytes each,
+// swizzled like the ring images -- are DMA'd once into one of two halo buffers,
+// and the nine taps read their A fragments from it at a pixel offset of
+// kh * (W + 2) + kw.  Only W goes through the per-step ring.  Halo pixels per
+// buffer: HQ DMA instructions per wave x 4 waves x 8 pixels.
+template <int BM>
+constexpr int kHaloHQ = BM == 64 ? 4 : 8;
+template <int BM, int BN, int STAGES, int KIND>
+constexpr int kLdsBytes = KIND == kConvHalo ? STAGES * BN * 128 + 2 * kHaloHQ<BM> * 32 * 128 + 16
+                                            : STAGES * (BM + BN) * 128 + 16;
+// Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
+// size, capped by what the tile's LDS ring allows (one wave per SIMD per block,
+// 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
+template <int BM, int BN, int STAGES, int KIND>
+constexpr int kMinWaves = std::max(1, std::min(BM * BN <= 64 * 64 ? 4 : BM * BN <= 128 * 64 ? 3 : 2,
+                                               (160 * 1024) / kLdsBytes<BM, BN, STAGES, KIND>));
 
 template <int MODE, int BM, int BN, int STAGES, int KIND>
-__global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(KArgs a) {
+__global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_kernel(KArgs a) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
+  constexpr bool HALO = KIND == kConvHalo;
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
   constexpr int CPR = RB / 16;             // chunks per image row
   constexpr int RPI = 64 / CPR;            // image rows per 1-KiB DMA instruction
-  constexpr int IMG = (BM + BN) * RB;      // bytes per stage
+  constexpr int IMG = (HALO ? BN : BM + BN) * RB;  // bytes per ring stage (halo: W only)
   constexpr int AQ = BM / RPI / 4, BQ = BN / RPI / 4;  // DMA instructions per wave per step
-  constexpr int QPS = AQ + BQ;
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * IMG + 16];
-  int* s_flag = reinterpret_cast<int*>(lds + STAGES * IMG);
+  constexpr int QPS = (HALO ? 0 : AQ) + BQ;
+  constexpr int HQ = HALO ? kHaloHQ<BM> : 1;          // halo DMA instructions per wave per block
+  constexpr int HBUF = HALO ? HQ * 4 * RPI * RB : 0;  // bytes per halo buffer
+  constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND>;
+  static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
+  static_assert(!HALO || (STAGES == 3 && RPI == 8), "halo: 9 taps unrolled over a 3-stage ring");
+  __shared__ __attribute__((aligned(16))) char lds[LDSB];
+  int* s_flag = reinterpret_cast<int*>(lds + LDSB - 16);
 
   const GemmDesc& d = a.d;
   // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
@@ -212,10 +240,21 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
   }
   const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int n0 = tn * BN;
+  // m_lim: first row past this tile's valid rows (halo bands end at the image)
+  int m0 = tm * BM, m_lim = d.M, h_img = 0, h_oy0 = 0;
+  if constexpr (HALO) {
+    h_img = tm / a.h_nb;
+    h_oy0 = (tm - h_img * a.h_nb) * a.h_th;
+    m0 = (h_img * d.OH + h_oy0) * d.OW;
+    m_lim = m0 + min(a.h_th, d.OH - h_oy0) * d.OW;
+  }
   const int kbeg = blockIdx.y * a.k_per_split;
   const int kend = min(d.Kpad, kbeg + a.k_per_split);
-  const int nsteps = (kend - kbeg) / ESTEP;
+  // halo: channel blocks [h_b0, h_b1) of this split-K slice, 9 taps each
+  const int h_b0 = HALO ? blockIdx.y * a.h_bps : 0;
+  const int h_b1 = HALO ? min(a.h_nblk, h_b0 + a.h_bps) : 0;
+  const int nsteps = HALO ? (h_b1 - h_b0) * 9 : (kend - kbeg) / ESTEP;
 
   const char* zeros = static_cast<const char*>(a.p.zeros);
   const AT* __restrict__ Ap = static_cast<const AT*>(a.p.A);
@@ -232,7 +271,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   // inside the image (0 for rows past M).  Indexed by the unrolled q only.
   uint32_t a_mask[AQ];
 #pragma unroll
-  for (int q = 0; q < AQ; ++q) {
+  for (int q = 0; q < (HALO ? 0 : AQ); ++q) {
     const int r = (wave * AQ + q) * RPI + lane / CPR;
     a_koff[q] = (slot ^ (r & (CPR - 1))) * EPC;
     const int m = m0 + r;
@@ -275,6 +314,48 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     b_src[q] = Wb + (size_t)(n0 + r) * row_bytes + c * 16;
   }
 
+  // Halo bookkeeping.  DMA side: lane of instruction wave*HQ + q fills pixel p
+  // (8 per instruction), slot s <- chunk s ^ (p & 7); h_src is its source for
+  // channel block 0 (block b adds b * ESTEP elements), zeros when p lies in the
+  // padding or past the halo.  Fragment side: h_row[i] = halo pixel of tap (0, 0)
+  // for this lane's row of A fragment i (rows past the band read pixel 0; their
+  // results are never stored).
+  [[maybe_unused]] const AT* h_src[HQ];
+  [[maybe_unused]] bool h_ok[HQ];
+  [[maybe_unused]] int h_row[BM / 32];
+  if constexpr (HALO) {
+#pragma unroll
+    for (int q = 0; q < HQ; ++q) {
+      const int p = (wave * HQ + q) * RPI + lane / CPR;
+      const int c = slot ^ (p & (CPR - 1));
+      const int hy = p / a.h_hwp, hx = p - hy * a.h_hwp;
+      const int iy = h_oy0 * d.stride - d.pad + hy, ix = hx - d.pad;
+      h_ok[q] = p < a.h_hp && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      h_src[q] = Ap + ((size_t)(h_img * d.H + (h_ok[q] ? iy : 0)) * d.W + (h_ok[q] ? ix : 0)) * d.Cin + c * EPC;
+    }
+    const int rows = m_lim - m0;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+      const int r = (wave >> 1) * (BM / 2) + i * 16 + (lane & 15);
+      const int ty = r / d.OW, tx = r - ty * d.OW;
+      h_row[i] = r < rows ? ty * d.stride * a.h_hwp + tx * d.stride : 0;
+    }
+  }
+  auto issue_halo = [&](int blk, int buf) {
+    if constexpr (HALO) {
+      char* dst = lds + STAGES * IMG + buf * HBUF;
+#pragma unroll
+      for (int q = 0; q < HQ; ++q) {
+        const char* src = h_ok[q] ? reinterpret_cast<const char*>(h_src[q] + (size_t)blk * ESTEP) : zeros;
+        SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * HQ + q) * 1024), 16, 0, 0);
+      }
+    }
+  };
+  // halo: scalar (block, tap) walk of the issued W steps; k = tap * Cin + c, so
+  // step (blk, tap) is W k-step tap * nblk + blk
+  int hw_blk = h_b0, hw_tap = 0;
+  int hw_blk_next = 0, hw_buf_next = 0;  // the halo issued at tap 7 of the current block
+
   // Cin >= k-step (one (kh, kw) tap per step): a scalar walk over (tap, channel
   // block), advanced once per issued step (issue() is called for steps 0, 1, 2 ...
   // in order): cu_cell = tap index, cu_off = element offset of (kh, kw, channel)
@@ -294,7 +375,17 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   auto issue = [&](int step, int stage) {
     const int k0 = kbeg + step * ESTEP;
     char* dst = lds + stage * IMG;
-    if constexpr (CONV) {
+    if constexpr (HALO) {
+      const int wstep = hw_tap * a.h_nblk + hw_blk;
+#pragma unroll
+      for (int q = 0; q < BQ; ++q)
+        SPI_DMA((const void*)(b_src[q] + (size_t)wstep * RB), (lds_ptr_t)(dst + (wave * BQ + q) * 1024), 16, 0, 0);
+      if (++hw_tap == 9) {
+        hw_tap = 0;
+        ++hw_blk;
+      }
+      return;
+    } else if constexpr (CONV) {
       if constexpr (TAP) {
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
@@ -328,7 +419,9 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
             if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W)
               src = reinterpret_cast<const char*>(a_base[q] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c);
           }
+#ifndef SPI_DIAG_NO_DMA_GEN  // diagnostic build: general convs (the stem) issue no DMA
           SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+#endif
         }
       }
     } else {
@@ -340,10 +433,12 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       }
     }
     // k-step byte offset inside a W row: RB bytes per step (advanced per issue).
+#ifdef SPI_DIAG_NO_DMA_GEN
+    if constexpr (KIND != kConvGen)
+#endif
 #pragma unroll
     for (int q = 0; q < BQ; ++q)
-      SPI_DMA((const void*)(b_src[q] + w_kb),
-                                       (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
+      SPI_DMA((const void*)(b_src[q] + w_kb), (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
     w_kb += RB;
   };
 
@@ -357,6 +452,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (HALO) issue_halo(h_b0, 0);  // lands before W step 0 (in-order vmcnt)
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) issue(s, s);
@@ -373,7 +469,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   // Tiles crossing N, or unaligned strides, take the per-element path from LDS.
   auto finish = [&](floatx4 (&v)[TI][TJ]) {
     using Out = typename TR::Out;
-    static_assert(BM * BN * 4 <= STAGES * IMG, "the C tile must fit the LDS ring");
+    static_assert(BM * BN * 4 <= LDSB - 16, "the C tile must fit the LDS");
     float* T = reinterpret_cast<float*>(lds);
     __syncthreads();  // every wave is done reading the ring
 #pragma unroll
@@ -435,7 +531,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
         if (a.p.res) {
 #pragma unroll
           for (int it = 0; it < CH; ++it) {
-            const int m = min(m0 + r0 + (c0 + it) * RSTEP, d.M - 1);
+            const int m = min(m0 + r0 + (c0 + it) * RSTEP, m_lim - 1);
             if constexpr (MODE == kF16X3S) {
               const _Float16* R = static_cast<const _Float16*>(a.p.res) + split_idx(m, nb, d.ldr);
               const half8 hi = *reinterpret_cast<const half8*>(R);
@@ -470,7 +566,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
 #pragma unroll
         for (int it = 0; it < CH; ++it) {
           const int m = m0 + r0 + (c0 + it) * RSTEP;
-          if (m >= d.M) continue;
+          if (m >= m_lim) continue;
           if (fmt == 2) {
             half8 hi, lo;
 #pragma unroll
@@ -500,7 +596,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     for (int e = 0; e < 8; ++e) b[e] = (a.p.bias && nb + e < d.N) ? a.p.bias[nb + e] : 0.f;
     for (int it = 0; it < ITEMS; ++it) {
       const int row = r0 + it * RSTEP, m = m0 + row;
-      if (m >= d.M) continue;
+      if (m >= m_lim) continue;
       float y[8];
       tile_vals(row, y);
       for (int e = 0; e < 8; ++e) {
@@ -531,11 +627,24 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   // One k-step; U = t % STAGES is a compile-time constant (the loop below is
   // unrolled by STAGES), so every stage offset -- M0 of the DMAs, the base of
   // the fragment reads -- is an immediate.
-  auto kstep = [&](int t, auto u_arg) {
+  // Halo steps also take the tap (a constant), whether this is the slice's last
+  // channel block, and that block's halo buffer.
+  auto kstep = [&](int t, auto u_arg, auto tap_arg, bool last_blk, const char* Hs) {
     const int U = u_arg;  // a constant when u_arg is a std::integral_constant
+    constexpr int TP = decltype(tap_arg)::value;
     SPI_STAMP(st_a);
     // Step t has landed once at most (issued steps after t) DMA groups remain.
-    if constexpr (STAGES == 4) {
+    // Halo: W step t + 1 is in flight, and at tap 8 of a block that has a
+    // successor the next block's halo too (issued at tap 7, before W step t + 2);
+    // the last step of the slice waits for everything.
+    if constexpr (HALO) {
+      if (last_blk && TP == 8)
+        dma_wait_barrier<0>();
+      else if (TP == 8)
+        dma_wait_barrier<BQ + HQ>();
+      else
+        dma_wait_barrier<BQ>();
+    } else if constexpr (STAGES == 4) {
       if (t + 2 < nsteps)
         dma_wait_barrier<2 * QPS>();
       else if (t + 1 < nsteps)
@@ -554,8 +663,20 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
     // All of this step's fragment reads go out first, then the next step's
     // DMAs (their issue cost overlaps the LDS latency), then the MFMAs.
     const char* As = lds + U * IMG;
-    const char* Bs = As + BM * RB;
+    const char* Bs = HALO ? As : As + BM * RB;
+    // A fragment i: image and row (halo: pixel of this tap, kh * (W + 2) + kw on)
+    const char* Ab = HALO ? Hs : As;
+    [[maybe_unused]] const int toff = HALO ? (TP / 3) * a.h_hwp + TP % 3 : 0;
+    auto arow = [&](int i) {
+      if constexpr (HALO)
+        return h_row[i] + toff;
+      else
+        return wm * WTM + i * 16 + fr;
+    };
     auto issue_next = [&] {
+      if constexpr (HALO) {
+        if (TP == 7 && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
+      }
       if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
     };
     if constexpr (MODE == (int)Prec::F16) {
@@ -564,7 +685,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
-          af[kk][i] = __builtin_bit_cast(half8, rd_chunk<RB>(As, wm * WTM + i * 16 + fr, kk * 4 + fq));
+          af[kk][i] = __builtin_bit_cast(half8, rd_chunk<RB>(Ab, arow(i), kk * 4 + fq));
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           bf[kk][j] = __builtin_bit_cast(half8, rd_chunk<RB>(Bs, wn * WTN + j * 16 + fr, kk * 4 + fq));
@@ -590,9 +711,9 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       half8 bh[TJ], bl[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const int row = wm * WTM + i * 16 + fr;
-        ar0[i] = rd_chunk<RB>(As, row, MODE == kF16X3S ? fq : 2 * fq);
-        ar1[i] = rd_chunk<RB>(As, row, MODE == kF16X3S ? 4 + fq : 2 * fq + 1);
+        const int row = arow(i);
+        ar0[i] = rd_chunk<RB>(Ab, row, MODE == kF16X3S ? fq : 2 * fq);
+        ar1[i] = rd_chunk<RB>(Ab, row, MODE == kF16X3S ? 4 + fq : 2 * fq + 1);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
@@ -628,9 +749,9 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
       floatx4 a0[TI], a1[TI], b0[TJ], b1[TJ];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const int row = wm * WTM + i * 16 + fr;
-        a0[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(As, row, 2 * fq));
-        a1[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(As, row, 2 * fq + 1));
+        const int row = arow(i);
+        a0[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Ab, row, 2 * fq));
+        a1[i] = __builtin_bit_cast(floatx4, rd_chunk<RB>(Ab, row, 2 * fq + 1));
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
@@ -671,23 +792,42 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  if constexpr (TAP) {
+  if constexpr (HALO) {
+    // one channel block per iteration, its 9 taps unrolled (stage = tap % 3)
+    const int nb = h_b1 - h_b0;
+    for (int j = 0; j < nb; ++j) {
+      const bool lb = j == nb - 1;
+      const char* Hs = lds + STAGES * IMG + (j & 1) * HBUF;
+      hw_blk_next = h_b0 + j + 1;
+      hw_buf_next = (j + 1) & 1;
+      const int t = j * 9;
+      kstep(t + 0, I0{}, std::integral_constant<int, 0>{}, lb, Hs);
+      kstep(t + 1, I1{}, std::integral_constant<int, 1>{}, lb, Hs);
+      kstep(t + 2, I2{}, std::integral_constant<int, 2>{}, lb, Hs);
+      kstep(t + 3, I0{}, std::integral_constant<int, 3>{}, lb, Hs);
+      kstep(t + 4, I1{}, std::integral_constant<int, 4>{}, lb, Hs);
+      kstep(t + 5, I2{}, std::integral_constant<int, 5>{}, lb, Hs);
+      kstep(t + 6, I0{}, std::integral_constant<int, 6>{}, lb, Hs);
+      kstep(t + 7, I1{}, std::integral_constant<int, 7>{}, lb, Hs);
+      kstep(t + 8, I2{}, std::integral_constant<int, 8>{}, lb, Hs);
+    }
+  } else if constexpr (TAP) {
     // unrolled by STAGES: stage offsets are immediates (the conv loop is short;
     // unrolling the large dense-GEMM bodies measured 1-2 % slower end to end)
     int t = 0;
     for (; t + STAGES <= nsteps; t += STAGES) {
-      kstep(t, I0{});
-      kstep(t + 1, I1{});
-      if constexpr (STAGES > 2) kstep(t + 2, I2{});
-      if constexpr (STAGES > 3) kstep(t + 3, I3{});
+      kstep(t, I0{}, I0{}, false, nullptr);
+      kstep(t + 1, I1{}, I0{}, false, nullptr);
+      if constexpr (STAGES > 2) kstep(t + 2, I2{}, I0{}, false, nullptr);
+      if constexpr (STAGES > 3) kstep(t + 3, I3{}, I0{}, false, nullptr);
     }
-    if (t < nsteps) kstep(t, I0{});
+    if (t < nsteps) kstep(t, I0{}, I0{}, false, nullptr);
     if constexpr (STAGES > 2)
-      if (t + 1 < nsteps) kstep(t + 1, I1{});
+      if (t + 1 < nsteps) kstep(t + 1, I1{}, I0{}, false, nullptr);
     if constexpr (STAGES > 3)
-      if (t + 2 < nsteps) kstep(t + 2, I2{});
+      if (t + 2 < nsteps) kstep(t + 2, I2{}, I0{}, false, nullptr);
   } else {
-    for (int t = 0; t < nsteps; ++t) kstep(t, t % STAGES);
+    for (int t = 0; t < nsteps; ++t) kstep(t, t % STAGES, I0{}, false, nullptr);
   }
 
   SPI_STAMP(st_d);
@@ -764,6 +904,8 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES>)) void gemm_kernel(
 
 struct Plan {
   int bm, bn, stages, splits, k_per_split;
+  // kConvHalo: output rows per band, bands per image, channel blocks per slice
+  int halo = 0, th = 0, nb = 0, bps = 0;
 };
 
 int estep_of(Prec prec) {
@@ -783,6 +925,7 @@ struct Knobs {
   bool latency = false;
   int target = 192;
   int max_split = 0, stages = 0;
+  int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
 };
 
 Knobs read_knobs() {
@@ -802,6 +945,7 @@ Knobs read_knobs() {
     if (std::strcmp(e, "latency") == 0) k.latency = true;
     if (std::strncmp(e, "tput:", 5) == 0) k.target = std::max(1, std::atoi(e + 5));
   }
+  if (const char* e = std::getenv("SPI_GEMM_HALO"); e && *e) k.halo = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SPI_GEMM_STAGES"); e && *e) k.stages = std::max(2, std::min(4, std::atoi(e)));
   return k;
@@ -824,6 +968,43 @@ Plan finish_plan(Plan pl, int ksteps, int ES) {
   return pl;
 }
 
+// kConvHalo plan for 3x3/s1/p1 convs with whole channel blocks (split activations
+// in F16X3): 128-row tiles when the output is wider than 32 pixels (the 56-wide
+// layers: two rows per band), else 64; as many whole output rows per band as fit
+// the tile and the halo buffer; split-K over channel blocks (64-row tiles only)
+// up to ~T workgroups.  halo = 0 when the conv is not eligible.
+Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
+  Plan no{};
+  const int ES = estep_of(prec);
+  if (!knobs().halo || knobs().forced || !d.conv || d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 ||
+      d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W)
+    return no;
+  const int bm = d.OW > 32 ? 128 : 64;
+  if ((knobs().halo == 2 && bm == 128) || (knobs().halo == 3 && bm == 64)) return no;  // experiments
+  const int cap = (bm == 64 ? 4 : 8) * 32;  // halo pixels per buffer (kHaloHQ x 4 waves x 8)
+  int th = std::min(bm / d.OW, d.OH);
+  while (th > 0 && (th + 2) * (d.W + 2) > cap) --th;
+  if (th == 0) return no;
+  const int imgs = d.M / (d.OH * d.OW);
+  const int nb = (d.OH + th - 1) / th, nblk = d.Cin / ES;
+  const int tiles = imgs * nb * (d.N / 64);
+  int sp = 1;
+  if (bm == 64 && tiles < T) sp = std::min((T + tiles - 1) / tiles, nblk);
+  const int bps = (nblk + sp - 1) / sp;
+  sp = (nblk + bps - 1) / bps;
+  Plan h{bm, 64, 3, sp, 0};
+  h.halo = 1;
+  h.th = th;
+  h.nb = nb;
+  h.bps = bps;
+  return h;
+}
+
+int plan_tiles(const GemmDesc& d, const Plan& pl) {
+  if (pl.halo) return d.M / (d.OH * d.OW) * pl.nb * ((d.N + pl.bn - 1) / pl.bn);
+  return ((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
+}
+
 // Plan rule (default): the largest tile that still yields >= T workgroups,
 // split-K only when even 64x64 tiles fall short (then to ~T workgroups, >= 6
 // k-steps per slice).  T = 192 measured best with 4 concurrent worker streams
@@ -838,6 +1019,7 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (k.forced) return finish_plan(k.plan, ksteps, ES);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
   const auto stages_for = [](int kt) { return kt >= 16 ? 3 : 2; };  // a deeper ring pays only on long K loops
+  if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
     const int T = k.target;
     if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES);
@@ -884,8 +1066,8 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.d = d;
   a.p = p;
   a.k_per_split = pl.k_per_split;
-  a.tiles_m = (d.M + pl.bm - 1) / pl.bm;
-  a.tiles = a.tiles_m * ((d.N + pl.bn - 1) / pl.bn);
+  a.tiles = plan_tiles(d, pl);
+  a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
   // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
@@ -893,6 +1075,21 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   a.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res)));
   const dim3 grid(a.tiles, pl.splits);
+  if (pl.halo) {
+    if constexpr (MODE != (int)Prec::F16X3) {  // fp32 A is split at fragment read: not a halo mode
+      a.h_th = pl.th;
+      a.h_nb = pl.nb;
+      a.h_hwp = d.W + 2 * d.pad;
+      a.h_hp = (pl.th + 2) * a.h_hwp;
+      a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
+      a.h_bps = pl.bps;
+      if (pl.bm == 128)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
+    }
+    return;
+  }
   if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(a, grid, s);
   else if (pl.bm == 128 && pl.stages == 2)
@@ -912,14 +1109,13 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
 size_t gemm_partial_floats(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
   if (pl.splits <= 1) return 0;
-  const size_t tiles = (size_t)((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
-  return tiles * pl.splits * pl.bm * pl.bn;
+  return (size_t)plan_tiles(d, pl) * pl.splits * pl.bm * pl.bn;
 }
 
 size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
   if (pl.splits <= 1) return 0;
-  return (size_t)((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
+  return (size_t)plan_tiles(d, pl);
 }
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }

@@ -558,7 +558,9 @@ GemmDesc linear_desc(const LinearW& L, int M, int lda, int ldc) {
 
 size_t Model::conv_partial(const ConvW& c, int B, int H, int W) const {
   int OH, OW;
-  return gemm_partial_floats(conv_desc(c, B, H, W, OH, OW), prec_);
+  GemmDesc d = conv_desc(c, B, H, W, OH, OW);
+  d.a_split = split_ && &c != &stem_;  // as run_conv: the plan (halo, split-K) depends on it
+  return gemm_partial_floats(d, prec_);
 }
 
 size_t Model::linear_partial(const LinearW& L, int M) const {

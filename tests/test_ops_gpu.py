@@ -56,7 +56,11 @@ def test_gemm_bias_residual_act(ops, prec, M, N, K, act):
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("B,H,cin,cout,k,stride", [(2, 224, 3, 64, 7, 2), (3, 56, 64, 64, 3, 1), (2, 56, 64, 128, 3, 2),
                                                    (2, 14, 256, 512, 1, 2), (4, 7, 512, 512, 3, 1),
-                                                   (1, 9, 16, 24, 3, 1)])
+                                                   (1, 9, 16, 24, 3, 1),
+                                                   # halo-band convs (kConvHalo): partial last band,
+                                                   # odd sizes, 3-row bands, split-K over channel blocks
+                                                   (2, 14, 128, 128, 3, 1), (2, 13, 64, 64, 3, 1),
+                                                   (2, 40, 64, 64, 3, 1), (1, 28, 128, 256, 3, 1)])
 def test_conv2d_nhwc(ops, prec, B, H, cin, cout, k, stride):
     g = torch.Generator().manual_seed(B * 1000 + H + cin + cout)
     x = torch.rand(B, cin, H, H, generator=g)
@@ -128,7 +132,9 @@ def test_layernorm(ops, prec, rows, D, eps):
 
 @pytest.mark.parametrize("B,H,cin,cout,k,stride,res", [(3, 56, 64, 64, 3, 1, True), (2, 56, 64, 128, 3, 2, False),
                                                        (2, 28, 128, 128, 3, 1, True), (2, 14, 256, 512, 1, 2, False),
-                                                       (4, 7, 512, 512, 3, 1, True), (1, 9, 32, 96, 3, 1, True)])
+                                                       (4, 7, 512, 512, 3, 1, True), (1, 9, 32, 96, 3, 1, True),
+                                                       (2, 14, 128, 128, 3, 1, True), (2, 13, 64, 64, 3, 1, True),
+                                                       (2, 40, 64, 64, 3, 1, False), (1, 9, 32, 128, 3, 1, True)])
 def test_conv2d_split_layout(ops, B, H, cin, cout, k, stride, res):
     """Split A / residual / output conv (the tap-walk kernel of every fp16x3 ResNet conv
     but the stem) vs an fp32 conv on the values the split layout holds."""
