@@ -185,7 +185,7 @@ constexpr bool kSplitK = BM == 64 && BN == 64;
 // k-step: scalar tap walk + per-row tap mask); conv in general (per-chunk taps:
 // the stem); 3x3/s1/p1 conv from an LDS-resident input band (kConvHalo, below).
 // Separate instantiations keep each kind's loop free of the others.
-enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3 };
+enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS = 4 };
 
 // kConvHalo.  An implicit-GEMM conv stages each (tap, channel block) A tile
 // separately: every input pixel crosses the CU nine times, and the vector-memory
@@ -197,11 +197,15 @@ enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3 };
 // and the nine taps read their A fragments from it at a pixel offset of
 // kh * (W + 2) + kw.  Only W goes through the per-step ring.  Halo pixels per
 // buffer: HQ DMA instructions per wave x 4 waves x 8 pixels.
-template <int BM>
-constexpr int kHaloHQ = BM == 64 ? 4 : 8;
+// kConvHaloS: the 64-row kind with 96-pixel buffers (14- and 7-wide layers):
+// 48 KiB of LDS instead of 56, three workgroups per CU instead of two.
+template <int BM, int KIND>
+constexpr int kHaloHQ = KIND == kConvHaloS ? 3 : BM == 64 ? 4 : 8;
+template <int KIND>
+constexpr bool kIsHalo = KIND == kConvHalo || KIND == kConvHaloS;
 template <int BM, int BN, int STAGES, int KIND>
-constexpr int kLdsBytes = KIND == kConvHalo ? STAGES * BN * 128 + 2 * kHaloHQ<BM> * 32 * 128 + 16
-                                            : STAGES * (BM + BN) * 128 + 16;
+constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND> * 32 * 128 + 16
+                                        : STAGES * (BM + BN) * 128 + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
 // size, capped by what the tile's LDS ring allows (one wave per SIMD per block,
 // 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
@@ -213,7 +217,7 @@ template <int MODE, int BM, int BN, int STAGES, int KIND>
 __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_kernel(KArgs a) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
-  constexpr bool HALO = KIND == kConvHalo;
+  constexpr bool HALO = kIsHalo<KIND>;
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
@@ -222,11 +226,11 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   constexpr int IMG = (HALO ? BN : BM + BN) * RB;  // bytes per ring stage (halo: W only)
   constexpr int AQ = BM / RPI / 4, BQ = BN / RPI / 4;  // DMA instructions per wave per step
   constexpr int QPS = (HALO ? 0 : AQ) + BQ;
-  constexpr int HQ = HALO ? kHaloHQ<BM> : 1;          // halo DMA instructions per wave per block
+  constexpr int HQ = HALO ? kHaloHQ<BM, KIND> : 1;          // halo DMA instructions per wave per block
   constexpr int HBUF = HALO ? HQ * 4 * RPI * RB : 0;  // bytes per halo buffer
   constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND>;
   static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
-  static_assert(!HALO || (STAGES == 3 && RPI == 8), "halo: 9 taps unrolled over a 3-stage ring");
+  static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
   int* s_flag = reinterpret_cast<int*>(lds + LDSB - 16);
 
@@ -638,12 +642,18 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
     // successor the next block's halo too (issued at tap 7, before W step t + 2);
     // the last step of the slice waits for everything.
     if constexpr (HALO) {
-      if (last_blk && TP == 8)
-        dma_wait_barrier<0>();
-      else if (TP == 8)
-        dma_wait_barrier<BQ + HQ>();
+      // G W groups in flight behind step t (fewer near the slice's end); the next
+      // block's halo goes out at tap 10 - STAGES (before W step t + STAGES - 1 =
+      // that block's tap 0), so the waits of the taps after it allow it too
+      constexpr int G = STAGES - 2;
+      constexpr int GL = G < 8 - TP ? G : 8 - TP;
+      constexpr bool XH = TP >= 11 - STAGES;
+      if (last_blk)
+        dma_wait_barrier<GL * BQ>();
+      else if (XH)
+        dma_wait_barrier<G * BQ + HQ>();
       else
-        dma_wait_barrier<BQ>();
+        dma_wait_barrier<G * BQ>();
     } else if constexpr (STAGES == 4) {
       if (t + 2 < nsteps)
         dma_wait_barrier<2 * QPS>();
@@ -675,7 +685,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
     };
     auto issue_next = [&] {
       if constexpr (HALO) {
-        if (TP == 7 && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
+        if (TP == 10 - STAGES && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
       }
       if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
     };
@@ -793,23 +803,42 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
   if constexpr (HALO) {
-    // one channel block per iteration, its 9 taps unrolled (stage = tap % 3)
+    // one channel block per iteration, its 9 taps unrolled (3 stages: stage =
+    // tap % 3, a constant; deeper rings: a scalar stage counter)
     const int nb = h_b1 - h_b0;
+    int u = 0;
     for (int j = 0; j < nb; ++j) {
       const bool lb = j == nb - 1;
       const char* Hs = lds + STAGES * IMG + (j & 1) * HBUF;
       hw_blk_next = h_b0 + j + 1;
       hw_buf_next = (j + 1) & 1;
       const int t = j * 9;
-      kstep(t + 0, I0{}, std::integral_constant<int, 0>{}, lb, Hs);
-      kstep(t + 1, I1{}, std::integral_constant<int, 1>{}, lb, Hs);
-      kstep(t + 2, I2{}, std::integral_constant<int, 2>{}, lb, Hs);
-      kstep(t + 3, I0{}, std::integral_constant<int, 3>{}, lb, Hs);
-      kstep(t + 4, I1{}, std::integral_constant<int, 4>{}, lb, Hs);
-      kstep(t + 5, I2{}, std::integral_constant<int, 5>{}, lb, Hs);
-      kstep(t + 6, I0{}, std::integral_constant<int, 6>{}, lb, Hs);
-      kstep(t + 7, I1{}, std::integral_constant<int, 7>{}, lb, Hs);
-      kstep(t + 8, I2{}, std::integral_constant<int, 8>{}, lb, Hs);
+      if constexpr (STAGES == 3) {
+        kstep(t + 0, I0{}, std::integral_constant<int, 0>{}, lb, Hs);
+        kstep(t + 1, I1{}, std::integral_constant<int, 1>{}, lb, Hs);
+        kstep(t + 2, I2{}, std::integral_constant<int, 2>{}, lb, Hs);
+        kstep(t + 3, I0{}, std::integral_constant<int, 3>{}, lb, Hs);
+        kstep(t + 4, I1{}, std::integral_constant<int, 4>{}, lb, Hs);
+        kstep(t + 5, I2{}, std::integral_constant<int, 5>{}, lb, Hs);
+        kstep(t + 6, I0{}, std::integral_constant<int, 6>{}, lb, Hs);
+        kstep(t + 7, I1{}, std::integral_constant<int, 7>{}, lb, Hs);
+        kstep(t + 8, I2{}, std::integral_constant<int, 8>{}, lb, Hs);
+      } else {
+        auto nx = [&] {
+          const int v = u;
+          u = u + 1 == STAGES ? 0 : u + 1;
+          return v;
+        };
+        kstep(t + 0, nx(), std::integral_constant<int, 0>{}, lb, Hs);
+        kstep(t + 1, nx(), std::integral_constant<int, 1>{}, lb, Hs);
+        kstep(t + 2, nx(), std::integral_constant<int, 2>{}, lb, Hs);
+        kstep(t + 3, nx(), std::integral_constant<int, 3>{}, lb, Hs);
+        kstep(t + 4, nx(), std::integral_constant<int, 4>{}, lb, Hs);
+        kstep(t + 5, nx(), std::integral_constant<int, 5>{}, lb, Hs);
+        kstep(t + 6, nx(), std::integral_constant<int, 6>{}, lb, Hs);
+        kstep(t + 7, nx(), std::integral_constant<int, 7>{}, lb, Hs);
+        kstep(t + 8, nx(), std::integral_constant<int, 8>{}, lb, Hs);
+      }
     }
   } else if constexpr (TAP) {
     // unrolled by STAGES: stage offsets are immediates (the conv loop is short;
@@ -926,6 +955,7 @@ struct Knobs {
   int target = 192;
   int max_split = 0, stages = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
+  int halo_stages = 3, halo_minh = 14;  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
 
 Knobs read_knobs() {
@@ -946,6 +976,8 @@ Knobs read_knobs() {
     if (std::strncmp(e, "tput:", 5) == 0) k.target = std::max(1, std::atoi(e + 5));
   }
   if (const char* e = std::getenv("SPI_GEMM_HALO"); e && *e) k.halo = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
+  if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SPI_GEMM_STAGES"); e && *e) k.stages = std::max(2, std::min(4, std::atoi(e)));
   return k;
@@ -977,14 +1009,15 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
   Plan no{};
   const int ES = estep_of(prec);
   if (!knobs().halo || knobs().forced || !d.conv || d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 ||
-      d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W)
+      d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W ||
+      d.OH < knobs().halo_minh)
     return no;
   const int bm = d.OW > 32 ? 128 : 64;
-  if ((knobs().halo == 2 && bm == 128) || (knobs().halo == 3 && bm == 64)) return no;  // experiments
   const int cap = (bm == 64 ? 4 : 8) * 32;  // halo pixels per buffer (kHaloHQ x 4 waves x 8)
   int th = std::min(bm / d.OW, d.OH);
   while (th > 0 && (th + 2) * (d.W + 2) > cap) --th;
   if (th == 0) return no;
+  const bool small = bm == 64 && (th + 2) * (d.W + 2) <= 3 * 32;  // kConvHaloS
   const int imgs = d.M / (d.OH * d.OW);
   const int nb = (d.OH + th - 1) / th, nblk = d.Cin / ES;
   const int tiles = imgs * nb * (d.N / 64);
@@ -992,8 +1025,8 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
   if (bm == 64 && tiles < T) sp = std::min((T + tiles - 1) / tiles, nblk);
   const int bps = (nblk + sp - 1) / sp;
   sp = (nblk + bps - 1) / bps;
-  Plan h{bm, 64, 3, sp, 0};
-  h.halo = 1;
+  Plan h{bm, 64, knobs().halo_stages, sp, 0};
+  h.halo = small ? 2 : 1;
   h.th = th;
   h.nb = nb;
   h.bps = bps;
@@ -1083,8 +1116,16 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
       a.h_hp = (pl.th + 2) * a.h_hwp;
       a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
       a.h_bps = pl.bps;
-      if (pl.bm == 128)
+      if (pl.bm == 128 && pl.stages == 4)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 4, kConvHalo>), grid, dim3(256), 0, s, a);
+      else if (pl.bm == 128)
         hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
+      else if (pl.halo == 2 && pl.stages == 4)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHaloS>), grid, dim3(256), 0, s, a);
+      else if (pl.halo == 2)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, a);
+      else if (pl.stages == 4)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHalo>), grid, dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
     }
