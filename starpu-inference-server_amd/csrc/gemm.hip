@@ -83,6 +83,7 @@ struct KArgs {
   int kw_mul;       // ceil(65536 / KW): cell / KW == (cell * kw_mul) >> 16 for cell < 2^12
   int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
   int vec_ok;       // C / residual rows allow 16-byte vectors of 8 elements (epilogue)
+  int xg_m, xg_n;   // XCD rectangles: tile rows in xg_m groups x tile columns in xg_n groups
   // halo conv (kConvHalo): tiles are bands of h_th output rows x the full width of
   // one image; h_nb bands per image; the band's input rows (+1 pixel of padding
   // around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel blocks,
@@ -243,7 +244,26 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
     const int nwg = a.tiles, q = nwg >> 3, r = nwg & 7, x = tile & 7, l = tile >> 3;
     if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
   }
-  const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
+  // Tile of linear index `tile`: the tile grid is cut into xg_m x xg_n
+  // rectangles (row groups i-major), each walked with tm fastest; the chunk of
+  // consecutive indices an XCD receives is then (about) one rectangle, so each
+  // A row block is fetched by xg_n XCD L2s and each W column block by xg_m
+  // (xg_m = 1: every XCD reads all of A -- the plain column-major order).
+  int tm, tn;
+  {
+    const int TM = a.tiles_m, TN = a.tiles / a.tiles_m, gm = a.xg_m, gn = a.xg_n;
+    int i = 0;
+    while (i + 1 < gm && ((i + 1) * TM / gm) * TN <= tile) ++i;
+    const int mlo = i * TM / gm, mi = (i + 1) * TM / gm - mlo;
+    const int l2 = tile - mlo * TN;  // index inside row group i: mi x TN tiles
+    const int c = l2 / mi;           // which tile column block it falls in
+    int j = 0;
+    while (j + 1 < gn && (j + 1) * TN / gn <= c) ++j;
+    const int nlo = j * TN / gn;
+    const int loc = l2 - mi * nlo;
+    tm = mlo + loc % mi;
+    tn = nlo + loc / mi;
+  }
   const int n0 = tn * BN;
   // m_lim: first row past this tile's valid rows (halo bands end at the image)
   int m0 = tm * BM, m_lim = d.M, h_img = 0, h_oy0 = 0;
@@ -955,7 +975,8 @@ struct Knobs {
   int target = 192;
   int max_split = 0, stages = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
-  int halo_stages = 3, halo_minh = 14;  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
+  int halo_stages = 3, halo_minh = 14;
+  int xcd2d = 1;  // 2-D tile -> XCD rectangles (xcd_groups)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
 
 Knobs read_knobs() {
@@ -976,6 +997,7 @@ Knobs read_knobs() {
     if (std::strncmp(e, "tput:", 5) == 0) k.target = std::max(1, std::atoi(e + 5));
   }
   if (const char* e = std::getenv("SPI_GEMM_HALO"); e && *e) k.halo = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_XCD2D"); e && *e) k.xcd2d = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
@@ -1031,6 +1053,30 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
   h.nb = nb;
   h.bps = bps;
   return h;
+}
+
+// XCD rectangles (gemm_kernel's tile decode): the row x column group split
+// gm x gn (gm * gn = 8, the XCDs) that minimises the bytes the XCDs' L2s fetch,
+// A * gn + W * gm (A: the activation bytes a tile row block reads -- the input
+// image for convs; W: the packed weights).  SPI_GEMM_XCD2D=0: gm = 1.
+void xcd_groups(const GemmDesc& d, Prec prec, int TM, int TN, int& gm, int& gn) {
+  gm = 1;
+  gn = std::min(8, TN);
+  if (!knobs().xcd2d || TM * TN < 16) return;
+  const double ea = prec == Prec::F16 ? 2 : 4, ew = prec == Prec::F16 ? 2 : 4;
+  const double A = d.conv ? (double)(d.M / (d.OH * d.OW)) * d.H * d.W * d.Cin * ea : (double)d.M * d.K * ea;
+  const double W = (double)d.N * d.Kpad * ew;
+  double best = 1e300;
+  for (int m = 1; m <= 8; m *= 2) {
+    const int n = 8 / m;
+    if (m > TM || n > TN) continue;
+    const double cost = A * n + W * m;
+    if (cost < best) {
+      best = cost;
+      gm = m;
+      gn = n;
+    }
+  }
 }
 
 int plan_tiles(const GemmDesc& d, const Plan& pl) {
@@ -1101,6 +1147,7 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.k_per_split = pl.k_per_split;
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
+  xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, a.tiles_m, a.tiles / a.tiles_m, a.xg_m, a.xg_n);
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
   // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
