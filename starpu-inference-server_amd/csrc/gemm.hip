@@ -72,6 +72,15 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
 #else
 #define SPI_DMA(src, dst, sz, off, aux) __builtin_amdgcn_global_load_lds(src, dst, sz, off, aux)
 #endif
+// Diagnostic build -DSPI_DIAG_L2A: every A-operand DMA reads from the first 64 KiB
+// of A (same instruction count and addressing work, almost no L2-miss traffic);
+// timed against the real kernel it separates memory-side traffic from the rest.
+#ifdef SPI_DIAG_L2A
+#define SPI_A_SRC(ptr_) \
+  (reinterpret_cast<const char*>(a.p.A) + ((reinterpret_cast<const char*>(ptr_) - reinterpret_cast<const char*>(a.p.A)) & 0xFFF0))
+#else
+#define SPI_A_SRC(ptr_) (ptr_)
+#endif
 
 struct KArgs {
   GemmDesc d;
@@ -371,7 +380,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 #pragma unroll
       for (int q = 0; q < HQ; ++q) {
         const char* src = h_ok[q] ? reinterpret_cast<const char*>(h_src[q] + (size_t)blk * ESTEP) : zeros;
-        SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * HQ + q) * 1024), 16, 0, 0);
+        SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * HQ + q) * 1024), 16, 0, 0);
       }
     }
   };
@@ -415,7 +424,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
         for (int q = 0; q < AQ; ++q) {
           const bool ok = (a_mask[q] >> cu_cell) & 1u;
           const char* src = ok ? reinterpret_cast<const char*>(a_src[q] + cu_off) : zeros;
-          SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
         // advance one k-step: next channel block, or the next tap (next pixel,
         // or the next filter row: W - KW + 1 pixels on)
@@ -444,7 +453,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
               src = reinterpret_cast<const char*>(a_base[q] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c);
           }
 #ifndef SPI_DIAG_NO_DMA_GEN  // diagnostic build: general convs (the stem) issue no DMA
-          SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
 #endif
         }
       }
@@ -453,7 +462,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
       for (int q = 0; q < AQ; ++q) {
         const int k = k0 + a_koff[q];
         const char* src = (a_ok[q] && k < d.K) ? reinterpret_cast<const char*>(a_pix[q] + k) : zeros;
-        SPI_DMA((const void*)src, (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+        SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
     // k-step byte offset inside a W row: RB bytes per step (advanced per issue).
