@@ -75,6 +75,26 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
 // Diagnostic build -DSPI_DIAG_L2A: every A-operand DMA reads from the first 64 KiB
 // of A (same instruction count and addressing work, almost no L2-miss traffic);
 // timed against the real kernel it separates memory-side traffic from the rest.
+// Diagnostic builds -DSPI_DIAG_NO_DMA_A / _W: drop only the A-operand (incl.
+// halo) or only the weight DMAs.
+#ifdef SPI_DIAG_NO_DMA_A
+#define SPI_DMA_A(src, dst, sz, off, aux) \
+  do {                                    \
+    (void)(src);                          \
+    (void)(dst);                          \
+  } while (0)
+#else
+#define SPI_DMA_A SPI_DMA
+#endif
+#ifdef SPI_DIAG_NO_DMA_W
+#define SPI_DMA_W(src, dst, sz, off, aux) \
+  do {                                    \
+    (void)(src);                          \
+    (void)(dst);                          \
+  } while (0)
+#else
+#define SPI_DMA_W SPI_DMA
+#endif
 #ifdef SPI_DIAG_L2A
 #define SPI_A_SRC(ptr_) \
   (reinterpret_cast<const char*>(a.p.A) + ((reinterpret_cast<const char*>(ptr_) - reinterpret_cast<const char*>(a.p.A)) & 0xFFF0))
@@ -380,7 +400,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 #pragma unroll
       for (int q = 0; q < HQ; ++q) {
         const char* src = h_ok[q] ? reinterpret_cast<const char*>(h_src[q] + (size_t)blk * ESTEP) : zeros;
-        SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * HQ + q) * 1024), 16, 0, 0);
+        SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * HQ + q) * 1024), 16, 0, 0);
       }
     }
   };
@@ -412,7 +432,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
       const int wstep = hw_tap * a.h_nblk + hw_blk;
 #pragma unroll
       for (int q = 0; q < BQ; ++q)
-        SPI_DMA((const void*)(b_src[q] + (size_t)wstep * RB), (lds_ptr_t)(dst + (wave * BQ + q) * 1024), 16, 0, 0);
+        SPI_DMA_W((const void*)(b_src[q] + (size_t)wstep * RB), (lds_ptr_t)(dst + (wave * BQ + q) * 1024), 16, 0, 0);
       if (++hw_tap == 9) {
         hw_tap = 0;
         ++hw_blk;
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
         for (int q = 0; q < AQ; ++q) {
           const bool ok = (a_mask[q] >> cu_cell) & 1u;
           const char* src = ok ? reinterpret_cast<const char*>(a_src[q] + cu_off) : zeros;
-          SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
         // advance one k-step: next channel block, or the next tap (next pixel,
         // or the next filter row: W - KW + 1 pixels on)
@@ -453,7 +473,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
               src = reinterpret_cast<const char*>(a_base[q] + ((size_t)(ih * d.W + iw) << a.cin_shift) + c);
           }
 #ifndef SPI_DIAG_NO_DMA_GEN  // diagnostic build: general convs (the stem) issue no DMA
-          SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+          SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
 #endif
         }
       }
@@ -462,7 +482,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
       for (int q = 0; q < AQ; ++q) {
         const int k = k0 + a_koff[q];
         const char* src = (a_ok[q] && k < d.K) ? reinterpret_cast<const char*>(a_pix[q] + k) : zeros;
-        SPI_DMA((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
+        SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
     }
     // k-step byte offset inside a W row: RB bytes per step (advanced per issue).
@@ -471,7 +491,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 #endif
 #pragma unroll
     for (int q = 0; q < BQ; ++q)
-      SPI_DMA((const void*)(b_src[q] + w_kb), (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
+      SPI_DMA_W((const void*)(b_src[q] + w_kb), (lds_ptr_t)(dst + BM * RB + (wave * BQ + q) * 1024), 16, 0, 0);
     w_kb += RB;
   };
 
