@@ -70,14 +70,20 @@ enum spi_interface_id {
   SPI_STARPU_VARIABLE_INTERFACE_ID = 5
 };
 
+/* Field widths: StarPU 1.4 declares the vector's nx (and slice_base) size_t --
+ * its register call takes `size_t nx`, which the reference's own link-time
+ * override of starpu_vector_data_register has to match exactly
+ * (tests/support/starpu_task_submit_override.cpp:117-119; the Dockerfile pins
+ * StarPU 1.4.8, Dockerfile:58).  A resize writes the full 8 bytes
+ * (resize_starpu_vector_interface, starpu_vector_resize_utils.hpp:19-64). */
 typedef struct spi_vector_interface {
   int32_t id; /* enum starpu_data_interface_id */
   uintptr_t ptr;
   uintptr_t dev_handle;
   size_t offset;
-  uint32_t nx;
+  size_t nx;
   size_t elemsize;
-  uint32_t slice_base;
+  size_t slice_base;
   size_t allocsize;
 } spi_vector_interface;
 
@@ -261,6 +267,9 @@ spi_model* spi_model_create(int32_t device_id, const spi_model_config* config,
 void spi_model_destroy(spi_model* model);
 /* Device bytes of the packed weight blob. */
 size_t spi_model_weight_bytes(const spi_model* model);
+/* FNV-1a 64 digest of the packed weight blob (computed on the host at build
+ * time): identical inputs give identical digests, whichever thread built it. */
+uint64_t spi_model_weight_digest(const spi_model* model);
 /* Algorithmic FLOPs of one forward at the given batch (roofline numerator). */
 double spi_model_flops(const spi_model* model, int64_t batch);
 /* Short description ("resnet[2,2,2,2] basic f16 ..."). */

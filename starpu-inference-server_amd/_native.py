@@ -61,9 +61,9 @@ class VectorInterface(C.Structure):
         ("ptr", C.c_size_t),
         ("dev_handle", C.c_size_t),
         ("offset", C.c_size_t),
-        ("nx", C.c_uint32),
+        ("nx", C.c_size_t),
         ("elemsize", C.c_size_t),
-        ("slice_base", C.c_uint32),
+        ("slice_base", C.c_size_t),
         ("allocsize", C.c_size_t),
     ]
 
@@ -173,6 +173,7 @@ _PROTOS = {
                                       C.c_char_p, C.c_size_t]),
     "spi_model_destroy": (None, [C.c_void_p]),
     "spi_model_weight_bytes": (C.c_size_t, [C.c_void_p]),
+    "spi_model_weight_digest": (C.c_uint64, [C.c_void_p]),
     "spi_model_flops": (C.c_double, [C.c_void_p, C.c_int64]),
     "spi_model_describe": (C.c_char_p, [C.c_void_p]),
     "spi_model_set_graphs": (None, [C.c_void_p, C.c_int32]),

@@ -183,6 +183,10 @@ class ModelReplica:
     def weight_bytes(self) -> int:
         return lib.spi_model_weight_bytes(self.handle)
 
+    @property
+    def weight_digest(self) -> int:
+        return lib.spi_model_weight_digest(self.handle)
+
     def flops(self, batch: int) -> float:
         return lib.spi_model_flops(self.handle, batch)
 

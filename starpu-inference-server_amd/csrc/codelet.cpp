@@ -373,6 +373,7 @@ spi_model* spi_model_create(int32_t device_id, const spi_model_config* config, c
 
 void spi_model_destroy(spi_model* m) { delete m; }
 size_t spi_model_weight_bytes(const spi_model* m) { return m ? m->impl->weight_bytes() : 0; }
+uint64_t spi_model_weight_digest(const spi_model* m) { return m ? m->impl->weight_digest() : 0; }
 double spi_model_flops(const spi_model* m, int64_t b) { return m ? m->impl->flops(b) : 0.0; }
 const char* spi_model_describe(const spi_model* m) { return m ? m->impl->describe().c_str() : ""; }
 int spi_model_profile(spi_model* m, void* stream, int64_t batch, int64_t seq, const void* const* inputs,

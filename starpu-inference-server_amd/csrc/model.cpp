@@ -92,7 +92,9 @@ class Blob {
   std::vector<char> data_;
 };
 
-Blob* g_blob = nullptr;  // only used during construction (single thread)
+// The blob being packed by this thread's Model constructor.  thread_local so
+// replicas can be built concurrently (one per device, clone_model_to_gpus).
+thread_local Blob* g_blob = nullptr;
 
 // Pack a [N][K] fp32 matrix (row-major, K contiguous) into [Npad][Kpad] of the
 // compute type.  get(n, k) supplies element (n, k) in packed-k order.
@@ -276,6 +278,9 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
   g_blob = nullptr;
 
   blob_bytes_ = blob.data().size();
+  uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+  for (char c : blob.data()) h = (h ^ (uint8_t)c) * 1099511628211ull;
+  digest_ = h;
   if (device_ < 0) return;  // host-only replica: recognised and packed, never uploaded
   SPI_HIP(hipSetDevice(device_));
   if (blob_bytes_) {
@@ -323,6 +328,34 @@ void Model::build_resnet(const PMap& p) {
   fc_ = pack_linear_named(p, "fc", prec_);
   classes_ = fc_.n;
   feat_ = fc_.k;
+  // Channel chain: every conv must read exactly the channels its producer
+  // writes.  A grouped conv (ResNeXt, models/import_resnet.py variants) stores
+  // weight.shape[1] = C/groups, which would otherwise be packed as a dense conv
+  // over too few channels and give garbage without an error.
+  {
+    auto bad = [](const std::string& what) {
+      throw std::runtime_error("resnet: grouped/unsupported conv (" + what + ")");
+    };
+    int ch = stem_.cout;
+    for (size_t i = 0; i < blocks_.size(); ++i) {
+      const ResBlock& b = blocks_[i];
+      const std::string id = "block " + std::to_string(i);
+      if (b.c1.cin != ch) bad(id + " conv1 reads " + std::to_string(b.c1.cin) + " of " + std::to_string(ch) + " channels");
+      if (b.c2.cin != b.c1.cout) bad(id + " conv2 reads " + std::to_string(b.c2.cin) + " of " + std::to_string(b.c1.cout) + " channels");
+      int out = b.c2.cout;
+      if (bottleneck_) {
+        if (b.c3.cin != b.c2.cout) bad(id + " conv3 reads " + std::to_string(b.c3.cin) + " of " + std::to_string(b.c2.cout) + " channels");
+        out = b.c3.cout;
+      }
+      if (b.has_ds) {
+        if (b.ds.cin != ch || b.ds.cout != out) bad(id + " downsample shape");
+      } else if (ch != out) {
+        bad(id + " identity residual with " + std::to_string(ch) + " -> " + std::to_string(out) + " channels");
+      }
+      ch = out;
+    }
+    if (fc_.k != ch) bad("fc reads " + std::to_string(fc_.k) + " of " + std::to_string(ch) + " features");
+  }
   for (auto& b : blocks_) {
     const ConvW* cs[] = {&b.c1, &b.c2, &b.c3, &b.ds};
     for (const ConvW* c : cs)
@@ -882,8 +915,16 @@ void Model::forward(hipStream_t s, int B, int S, size_t n, const void* const* in
     auto it = w->graphs.find(key);
     if (it == w->graphs.end()) {
       SPI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      body(*w, B, S, s);
       hipGraph_t g = nullptr;
+      try {
+        body(*w, B, S, s);
+      } catch (...) {
+        // Leave the worker stream usable: end the capture before rethrowing,
+        // otherwise every later task on this stream fails.
+        if (hipStreamEndCapture(s, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        throw;
+      }
       SPI_HIP(hipStreamEndCapture(s, &g));
       hipGraphExec_t e = nullptr;
       SPI_HIP(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
@@ -900,6 +941,8 @@ void Model::forward(hipStream_t s, int B, int S, size_t n, const void* const* in
 }  // namespace spi
 
 namespace spi {
+
+thread_local std::vector<Model::OpRecord>* Model::prof_ = nullptr;
 
 void Model::op_begin(hipStream_t s, const std::string& name, double flops, double bytes) {
   OpRecord r{name, flops, bytes, nullptr, nullptr};

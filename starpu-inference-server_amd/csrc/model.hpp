@@ -60,6 +60,7 @@ class Model {
   bool f16() const { return f16_; }
   int max_batch() const { return max_batch_; }
   size_t weight_bytes() const { return blob_bytes_; }
+  uint64_t weight_digest() const { return digest_; }
   const std::string& describe() const { return desc_; }
   double flops(int64_t batch) const;
   void set_graphs(bool on) { graphs_ = on; }
@@ -120,6 +121,7 @@ class Model {
   std::vector<char> hblob_;
   void* dblob_ = nullptr;
   size_t blob_bytes_ = 0;
+  uint64_t digest_ = 0;
 
   // AFFINE
   float aff_scale_ = 1.f, aff_shift_ = 0.f;
@@ -143,7 +145,9 @@ class Model {
 
   std::mutex mu_;
   std::map<hipStream_t, std::unique_ptr<Workspace>> ws_;
-  std::vector<OpRecord>* prof_ = nullptr;  // set only inside profile()
+  // Set only inside profile(), on the profiling thread: forwards running on
+  // other worker threads at the same time never see it.
+  static thread_local std::vector<OpRecord>* prof_;
   void op_begin(hipStream_t s, const std::string& name, double flops, double bytes);
   void op_end(hipStream_t s);
   // Profiled launch (bytes = algorithmic traffic); a plain call when not profiling.

@@ -154,14 +154,14 @@ void spi_runtime::run(Worker* w) {
     for (int i = 0; i < ni; ++i) {
       const size_t es = spi_dtype_size(cfg.input_types[i]);
       ifaces[i] = spi_vector_interface{SPI_STARPU_VECTOR_INTERFACE_ID, (uintptr_t)w->d_in[i], 0, 0,
-                                       (uint32_t)(total * in_sample_bytes[i] / es), es, 0,
+                                       (size_t)(total * in_sample_bytes[i] / es), es, 0,
                                        (size_t)cfg.max_batch * in_sample_bytes[i]};
       buffers[i] = &ifaces[i];
     }
     for (int i = 0; i < no; ++i) {
       const size_t es = spi_dtype_size(cfg.output_types[i]);
       ifaces[ni + i] = spi_vector_interface{SPI_STARPU_VECTOR_INTERFACE_ID, (uintptr_t)w->d_out[i], 0, 0,
-                                            (uint32_t)(total * out_sample_bytes[i] / es), es, 0,
+                                            (size_t)(total * out_sample_bytes[i] / es), es, 0,
                                             (size_t)cfg.max_batch * out_sample_bytes[i]};
       buffers[ni + i] = &ifaces[ni + i];
     }

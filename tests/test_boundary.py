@@ -54,8 +54,7 @@ PROBE = r"""
 #define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 #define S(T) printf(#T " %zu\n", sizeof(T));
 int main(void) {
-  S(spi_vector_interface) F(spi_vector_interface, ptr) F(spi_vector_interface, nx)
-  F(spi_vector_interface, elemsize) F(spi_vector_interface, allocsize)
+  S(spi_vector_interface) F(spi_vector_interface, ptr) F(spi_vector_interface, nx) F(spi_vector_interface, elemsize) F(spi_vector_interface, slice_base) F(spi_vector_interface, allocsize)
   S(spi_variable_interface) F(spi_variable_interface, ptr) F(spi_variable_interface, elemsize)
   S(spi_tensor_view) S(spi_named_tensor) S(spi_model_config)
   S(spi_codelet_args) F(spi_codelet_args, dims) F(spi_codelet_args, input_types)
@@ -101,6 +100,12 @@ def test_buffer_byte_size(spi):
     assert spi.buffer_byte_size(vec) == 40
     vec.nx = 0
     assert spi.buffer_byte_size(vec) == 0
+    vec.nx = 1 << 40  # nx is size_t (StarPU 1.4): no 32-bit truncation
+    assert spi.buffer_byte_size(vec) == (1 << 40) * 8
+    # BufferByteSize.ThrowsWhenVectorSizeOverflows (unit_starpu_setup.cpp:2105-2124)
+    over = spi.make_vector_interface(0x1000, 2, 2**64 - 1)
+    with pytest.raises(spi.InferenceExecutionException, match="exceeds size_t capacity"):
+        spi.buffer_byte_size(over)
     bad = N.VariableInterface(3, 0, 0, 0, 4)  # CSR id: unsupported
     with pytest.raises(spi.InferenceExecutionException, match="Unsupported StarPU buffer interface id 3"):
         spi.buffer_byte_size(bad)
@@ -259,6 +264,53 @@ def test_recognition_errors(spi, zoo):
         spi.ModelReplica(Named(sd), -1, "fp16", image_size=64)
     with pytest.raises(spi.InferenceExecutionException, match="unrecognised model"):
         spi.ModelReplica(Named({"foo.weight": torch.zeros(2)}), -1, "fp16")
+
+
+def _named(d):
+    class Named(torch.nn.Module):
+        def named_parameters(self, *a, **k):
+            return iter([])
+
+        def named_buffers(self, *a, **k):
+            return iter(d.items())
+    return Named()
+
+
+def test_grouped_conv_resnext_is_rejected(spi, zoo):
+    """ResNeXt (grouped 3x3, models/import_resnet.py variants) stores weight.shape[1] = C/groups;
+    packing it as a dense conv would silently give garbage, so the channel chain is checked."""
+    m = zoo.resnet([1, 1, 1, 1], True, image=64)
+    sd = dict(m.state_dict())
+    w = sd["layer1.0.conv2.weight"]  # [64, 64, 3, 3] -> groups=8: [64, 8, 3, 3]
+    sd["layer1.0.conv2.weight"] = w[:, :8].clone()
+    with pytest.raises(spi.InferenceExecutionException, match="grouped/unsupported conv"):
+        spi.ModelReplica(_named(sd), -1, "fp16", image_size=64)
+    # an identity residual whose channels do not line up is rejected too
+    sd = dict(m.state_dict())
+    sd = {k: v for k, v in sd.items() if not k.startswith("layer1.0.downsample")}
+    with pytest.raises(spi.InferenceExecutionException, match="grouped/unsupported conv"):
+        spi.ModelReplica(_named(sd), -1, "fp16", image_size=64)
+
+
+def test_replicas_build_concurrently(spi, zoo):
+    """spi_model_create is re-entrant: replicas packed from several threads at once
+    (one per device, clone_model_to_gpus) equal the serially built one byte for byte."""
+    import threading
+    m = zoo.resnet([1, 1, 1, 1], False, image=64)
+    ref = spi.ModelReplica(m, -1, "fp16x3", image_size=64)
+    out = [None] * 4
+
+    def build(i):
+        out[i] = spi.ModelReplica(m, -1, "fp16x3", image_size=64)
+
+    ts = [threading.Thread(target=build, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(r is not None and r.weight_digest == ref.weight_digest for r in out)
+    other = spi.ModelReplica(m, -1, "fp16", image_size=64)
+    assert other.weight_digest != ref.weight_digest
 
 
 def test_torchscript_file_is_accepted(spi, zoo, tmp_path):
