@@ -15,7 +15,7 @@ from oracle.cpu_codelet import cpu_inference, normalized_max_error, top1_agreeme
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": 1e-5, "fp16": 1e-3, "fp16x3": 1e-3}
+TOL = {"fp32": 1e-5, "fp16": 1e-3, "fp16x3": 1e-5}  # fp16x3 measures 1.6e-6 .. 3.2e-6 (fp32-grade)
 # Plain fp16 operands on the random-init ResNets: rounding the MFMA operands
 # alone gives ~1.7e-3 normalised max error (CPU emulation: fp16 weights 1.4e-3,
 # fp16 activations 1.2e-3, both 1.67e-3 at ResNet-18 bs8@224).  That is the
@@ -54,7 +54,7 @@ def test_resnet18_small_image(spi, zoo, gpu, prec):
     err = normalized_max_error(got, ref)
     print(f"resnet18@64 {prec} err={err:.3e}")
     assert np.isfinite(got).all()
-    assert err < resnet_tol(prec) * 2
+    assert err < resnet_tol(prec)
     assert top1_agreement(got, ref) == 1.0
 
 
@@ -68,7 +68,7 @@ def test_resnet_bottleneck_small(spi, zoo, gpu, prec):
     got = hip_forward(spi, rep, [x], ref.shape)
     err = normalized_max_error(got, ref)
     print(f"resnet-bottleneck@64 {prec} err={err:.3e}")
-    assert err < (1e-2 if prec == "fp16" else resnet_tol(prec))  # 64x64 images: small logits, plain fp16 floor
+    assert err < resnet_tol(prec)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3"])
@@ -106,7 +106,7 @@ def test_bert_two_layers_masked(spi, zoo, gpu, prec):
     got = hip_forward(spi, rep, [ids, mask], ref.shape)
     err = normalized_max_error(got, ref)
     print(f"bert L2 S80 masked {prec} err={err:.3e}")
-    assert err < TOL[prec] * 2
+    assert err < TOL[prec]
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
@@ -134,7 +134,7 @@ def test_vit_small_seq197(spi, zoo, gpu, prec):
     got = hip_forward(spi, rep, [x], ref.shape)
     err = normalized_max_error(got, ref)
     print(f"vit-small S197 {prec} err={err:.3e}")
-    assert err < TOL[prec] * 2
+    assert err < TOL[prec]
 
 
 def test_affine_codelet_like_reference(spi, gpu):
@@ -176,6 +176,8 @@ def test_hip_matches_committed_golden_fixtures(spi, gpu, name, prec):
     rep = spi.ModelReplica(model, 0, prec, max_batch=2, **kw)
     got = hip_forward(spi, rep, inputs, ref.shape)
     err = normalized_max_error(got, ref)
-    tol = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 1e-2}[prec]
+    # plain fp16 operands: the north_star 1e-3 bar on BERT (8.6e-4 measured); the tiny random
+    # ResNets / ViT-D128 sit at their format floor (2.4e-3 / 1.1e-3), see TOL_RESNET_PLAIN_FP16
+    tol = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 1e-3 if name.startswith("bert") else TOL_RESNET_PLAIN_FP16}[prec]
     print(f"golden {name} {prec} err={err:.3e}")
     assert err < tol

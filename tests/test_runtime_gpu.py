@@ -136,3 +136,27 @@ def test_runtime_bs1_requests_batched_to_8(spi, zoo, rtmod):
     assert normalized_max_error(np.concatenate(ys), ref) < 1e-5
     assert sum(c.task_jobs for c in rt.completions) / len(rt.completions) > 1.5
     rt.close()
+
+
+def test_runtime_two_replicas_on_one_device(spi, zoo, rtmod):
+    """num_devices = 2 with device_ids [0, 0]: two weight replicas (clone_model_to_gpus,
+    per_device) served by their own workers from one eager queue -- the multi-device path
+    rehearsed on a one-GPU box.  Every task must match the oracle, whichever replica ran it."""
+    m = zoo.resnet18(image=64)
+    reps = spi.clone_model_to_gpus(m, [0, 0], precision="fp16x3", max_batch=4, image_size=64)
+    rt = rtmod.Runtime(reps, [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=4, workers_per_device=2)
+    rng = np.random.default_rng(5)
+    jobs = []
+    for rid in range(24):
+        x = rng.random((4, 3, 64, 64), dtype=np.float32)
+        y = np.full((4, 1000), np.nan, dtype=np.float32)
+        rt.submit(rid, [x], [y])
+        jobs.append((x, y))
+    rt.drain()
+    assert rt.stats() == (24, 0)
+    for x, y in jobs:
+        assert normalized_max_error(y, cpu_inference(m, [x])[0]) < 1e-5
+    by_worker = {c.worker_id for c in rt.completions}
+    # workers 0-1 serve replica 0, workers 2-3 replica 1
+    assert by_worker & {0, 1} and by_worker & {2, 3}
+    rt.close()
