@@ -138,7 +138,15 @@ class ModelReplica:
                  image_size: int = 0, eps: float = 0.0, affine: tuple[float, float] = (1.0, 0.0),
                  graphs: bool = False):
         if isinstance(module, str):
-            module = load_model(module)
+            # The reference's on-disk format: torch::jit::load + the C++ weight
+            # extractor in libspi_torch.so (inference_runner.cpp:243-275).
+            from .libtorch import TorchScriptModule
+            ts = TorchScriptModule(module)
+            rep = ts.replica(device_id, precision, max_batch, family=family, num_heads=num_heads, seq_len=seq_len,
+                             image_size=image_size, eps=eps, graphs=graphs)
+            self.__dict__.update(rep.__dict__)
+            rep.handle = None  # ownership moved to self
+            return
         tensors = named_tensors(module) if module is not None else []
         arr = (N.NamedTensor * max(1, len(tensors)))()
         keep = []
@@ -171,6 +179,18 @@ class ModelReplica:
         self.max_batch = max_batch
         if graphs:
             self.set_graphs(True)
+
+    @classmethod
+    def from_handle(cls, handle: int, device_id: int, precision: str, max_batch: int,
+                    graphs: bool = False) -> "ModelReplica":
+        self = cls.__new__(cls)
+        self.handle = C.c_void_p(handle)
+        self.device_id = device_id
+        self.precision = precision
+        self.max_batch = max_batch
+        if graphs:
+            self.set_graphs(True)
+        return self
 
     def set_graphs(self, on: bool) -> None:
         lib.spi_model_set_graphs(self.handle, 1 if on else 0)

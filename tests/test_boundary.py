@@ -20,9 +20,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
+def header_functions(pattern="*.h"):
     names = set()
-    for path in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for path in glob.glob(os.path.join(ROOT, "include", pattern)):
         for line in open(path):
             if line.lstrip().startswith(("typedef", "*", "/*", "#")):
                 continue
@@ -32,18 +32,27 @@ def header_functions():
     return names
 
 
-def test_library_exports_every_header_symbol(spi):
-    names = header_functions()
-    assert len(names) >= 36
-    out = subprocess.run(["nm", "-D", "--defined-only", spi._native.LIB_PATH], capture_output=True, text=True,
+def exported(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True, text=True,
                          check=True).stdout
-    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
-    missing = sorted(names - exported)
-    assert not missing, f"declared but not exported: {missing}"
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_library_exports_every_header_symbol(spi):
     import importlib
+    torch_names = header_functions("spi_torch.h")
+    names = header_functions() - torch_names
+    assert len(names) >= 36 and len(torch_names) >= 8
+    missing = sorted(names - exported(spi._native.LIB_PATH))
+    assert not missing, f"declared but not exported by libspi_hip.so: {missing}"
+    lt = importlib.import_module("starpu-inference-server_amd.libtorch")
+    missing = sorted(torch_names - exported(lt.LIB_PATH))
+    assert not missing, f"declared but not exported by libspi_torch.so: {missing}"
     importlib.import_module("starpu-inference-server_amd.runtime")  # binds include/spi_runtime.h
     for n in names:  # and every one is bound in ctypes
         assert n in spi._native._PROTOS or getattr(spi.lib, n).argtypes is not None, n
+    for n in torch_names:
+        assert n in lt._PROTOS, n
 
 
 PROBE = r"""
