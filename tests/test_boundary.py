@@ -73,6 +73,15 @@ int main(void) {
   S(spi_runtime_config) F(spi_runtime_config, models) F(spi_runtime_config, workers_per_device)
   F(spi_runtime_config, input_dims) F(spi_runtime_config, num_outputs) F(spi_runtime_config, output_elems)
   F(spi_runtime_config, coalesce_max_jobs) F(spi_runtime_config, coalesce_delay_us)
+  F(spi_runtime_config, pipeline_depth) F(spi_runtime_config, h2d_mode) F(spi_runtime_config, max_priority)
+  F(spi_runtime_config, batching)
+  S(spi_batching_config) F(spi_batching_config, exit_horizon_us) F(spi_batching_config, fill_high)
+  F(spi_batching_config, rho_low) S(spi_batching_pressure) F(spi_batching_pressure, congested)
+  S(spi_batching_state) F(spi_batching_state, last_update_ns)
+  S(spi_job_desc) F(spi_job_desc, batch) F(spi_job_desc, done) F(spi_job_desc, user)
+  S(spi_loadgen_config) F(spi_loadgen_config, segments) F(spi_loadgen_config, warmup_requests)
+  S(spi_loadgen_result) F(spi_loadgen_result, p50_queue_ms) F(spi_loadgen_result, error)
+  S(spi_schedule_segment)
   S(spi_job_timing) F(spi_job_timing, complete_ns) F(spi_job_timing, worker_id) F(spi_job_timing, task_jobs)
   return 0;
 }
@@ -90,6 +99,10 @@ def test_ctypes_layouts_match_the_c_header(spi, tmp_path):
     rt = importlib.import_module("starpu-inference-server_amd.runtime")
     N = spi._native
     types = {"spi_runtime_config": rt.RuntimeConfig, "spi_job_timing": rt.JobTiming,
+             "spi_batching_config": rt.BatchingConfig, "spi_batching_pressure": rt.BatchingPressure,
+             "spi_batching_state": rt.BatchingState, "spi_job_desc": rt.JobDesc,
+             "spi_loadgen_config": rt.LoadgenConfig, "spi_loadgen_result": rt.LoadgenResult,
+             "spi_schedule_segment": rt.ScheduleSegment,
              "spi_vector_interface": N.VectorInterface, "spi_variable_interface": N.VariableInterface,
              "spi_tensor_view": N.TensorView, "spi_named_tensor": N.NamedTensor, "spi_model_config": N.ModelConfig,
              "spi_codelet_args": N.CodeletArgs}

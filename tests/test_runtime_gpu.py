@@ -160,3 +160,102 @@ def test_runtime_two_replicas_on_one_device(spi, zoo, rtmod):
     # workers 0-1 serve replica 0, workers 2-3 replica 1
     assert by_worker & {0, 1} and by_worker & {2, 3}
     rt.close()
+
+
+@pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy"])
+def test_runtime_pipeline_with_small_slot_pool(spi, zoo, rtmod, h2d_mode):
+    """Pipeline depth 3 per worker over a 2-slot pool (fewer slots than workers x depth): the
+    worker must finalize its own finished tasks to free slots (SlotPoolBase::try_acquire /
+    acquire / release) -- every ragged job still matches its own forward."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=4, image_size=64)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=4, workers_per_device=2,
+                       pipeline_depth=3, slots_per_device=2, h2d_mode=h2d_mode, copy_threads=3)
+    rng = np.random.default_rng(8)
+    jobs = []
+    for rid in range(40):
+        b = 1 + rid % 4
+        x = rng.random((b, 3, 64, 64), dtype=np.float32)
+        y = np.full((b, 1000), np.nan, dtype=np.float32)
+        rt.submit(rid, [x], [y])
+        jobs.append((x, y))
+    rt.drain()
+    assert rt.stats() == (40, 0)
+    for x, y in jobs:
+        assert normalized_max_error(y, cpu_inference(m, [x])[0]) < 1e-5
+    rt.close()
+
+
+def test_runtime_fixed_worker_and_priority(spi, zoo, rtmod):
+    """assign_fixed_worker_if_needed (inference_task.cpp:824-842): pinned jobs run on their worker.
+    Priority (create_task, :690-753): queued jobs leave the queue highest priority first, and the
+    default priority is max(min_prio, max_prio - request_id)."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp32", max_batch=8, image_size=64)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=3)
+    x = np.random.default_rng(9).random((1, 3, 64, 64), dtype=np.float32)
+    ys = [np.zeros((1, 1000), np.float32) for _ in range(12)]
+    for i in range(12):
+        rt.submit(i, [x], [ys[i]], fixed_worker=i % 3)
+    rt.drain()
+    assert all(c.worker_id == c.request_id % 3 and c.status == 0 for c in rt.completions)
+    rt.close()
+
+    big = spi.ModelReplica(zoo.resnet152(), 0, "fp32", max_batch=8)  # ~ms per task: the queue fills behind it
+    rt = rtmod.Runtime([big], [((3, 224, 224), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=1,
+                       pipeline_depth=1, min_priority=-100, max_priority=100)
+    xb = np.random.default_rng(10).random((8, 3, 224, 224), dtype=np.float32)
+    yb = [np.zeros((8, 1000), np.float32) for _ in range(2)]
+    xs = np.random.default_rng(11).random((1, 3, 224, 224), dtype=np.float32)
+    small = [np.zeros((1, 1000), np.float32) for _ in range(6)]
+    rt.submit(100, [xb], [yb[0]])          # occupies the only worker
+    rt.submit(101, [xb], [yb[1]])          # queued behind it, so the next three queue too
+    for k, rid in enumerate([5, 3, 4]):     # default priorities 95, 97, 96
+        rt.submit(rid, [xs], [small[k]])
+    rt.submit(50, [xs], [small[3]], priority=-50)
+    rt.submit(51, [xs], [small[4]], priority=99)
+    rt.drain()
+    order = [c.request_id for c in sorted(rt.completions, key=lambda c: c.dequeue_ns)]
+    assert order[0] == 100
+    assert order[1:] == [51, 3, 4, 5, 101, 50]  # 51 (99) > 3 (97) > 4 > 5 > 101 (max(-100, 100-101)=-1) > 50 (-50)
+    rt.close()
+
+
+def test_runtime_adaptive_batching_under_load(spi, zoo, rtmod):
+    """AdaptiveBatchingStrategy in the runtime: bs1 requests under a backlog grow the target
+    (queue fill / in-flight pressure) and every merged job still gets its own rows back."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=8, image_size=64)
+    b = rtmod.batching_config("adaptive", min_batch=1, batch_limit=8, coalesce_timeout_us=200, congestion=True,
+                              tick_us=100, entry_horizon_us=400, exit_horizon_us=2000)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=2,
+                       max_queue=64, batching=b)
+    rng = np.random.default_rng(12)
+    xs = [rng.random((1, 3, 64, 64), dtype=np.float32) for _ in range(48)]
+    ys = [np.zeros((1, 1000), np.float32) for _ in range(48)]
+    for i in range(48):
+        rt.submit(i, [xs[i]], [ys[i]])
+    rt.drain()
+    assert rt.stats() == (48, 0)
+    ref = cpu_inference(m, [np.concatenate(xs)])[0]
+    assert normalized_max_error(np.concatenate(ys), ref) < 1e-5
+    assert max(c.task_batch for c in rt.completions) > 1
+    assert 1 <= rt.batch_target <= 8
+    rt.close()
+
+
+def test_runtime_loadgen_closed_and_open_loop(spi, zoo, rtmod):
+    """The C++ client loop: closed loop with k requests outstanding, and the open-loop
+    (delta_us, repeat) schedule of ci/perf/ci_perf_resnet.csv with a bounded queue."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=8, image_size=64, graphs=True)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=4,
+                       max_queue=32, coalesce_max_jobs=8, coalesce_delay_us=100)
+    x = np.random.default_rng(13).random((1, 3, 64, 64), dtype=np.float32)
+    r = rt.loadgen([x], requests=400, inflight=16, warmup=16)
+    assert r["completed"] == 400 and r["failed"] == 0 and r["inferences_per_s"] > 0
+    assert 0 < r["p50_ms"] <= r["p95_ms"] <= r["p99_ms"] <= r["max_ms"]
+    assert r["mean_task_batch"] >= 1
+    r = rt.loadgen([x], schedule=[(300, 50), (50, 100), (500, 20)])
+    assert r["completed"] + r["rejected"] == 170 and r["failed"] == 0
+    rt.close()
