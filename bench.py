@@ -1,35 +1,41 @@
 #!/usr/bin/env python3
 """MI355X inference-codelet benchmark (BASELINE.json metric: inferences/sec + p50 latency).
 
-Headline workload = BASELINE.json configs[1]: ResNet-18, batch 8 per task, fp16
-MFMA, one MI355X -- run in the parity-grade fp16x3 mode (split-fp16 MFMA,
-fp32-grade results; plain fp16 operands miss the 1e-3 bar on this network,
-DESIGN.md 3).  A *step* is one task per worker: each of the `--workers` workers
-of a GPU (STARPU_NWORKER_PER_CUDA=4, models/resnet18.yml:6) calls the HIP
-codelet (libspi_hip.so, through the C-ABI) on its own HIP stream over one
-synthetic batch already resident in HBM.
+Headline workload = BASELINE.json configs[1]: ResNet-18, batch 8 per task, fp16 MFMA, one
+MI355X -- run in the parity-grade fp16x3 mode (split-fp16 MFMA, fp32-grade results; plain fp16
+operands miss the 1e-3 bar on this network).  The `--workers` HIP worker streams
+of a GPU (STARPU_NWORKER_PER_CUDA=4, models/resnet18.yml:6) each call the HIP codelet
+(libspi_hip.so, through the C-ABI) on a synthetic batch already resident in HBM.  A *step* is
+`--tasks-per-step` codelet calls on every worker stream (default 8: 32 tasks = 256 images per GPU).
 
-Multi-GPU: one process per GPU (torch.distributed.run), one weight replica per
-device, tasks sharded across devices with no data-path collective
-("scaling": "weak"); a gloo barrier brackets the timed region and the time is
-the max over ranks; `value` = inferences of all ranks / that time.
+`value` = inferences of all ranks / (max over ranks of the barrier + device-sync bracketed time of
+exactly `--steps` steps), inputs resident in HBM.  Multi-GPU: one process per GPU
+(torch.distributed.run), one weight replica per device, tasks sharded across devices with no
+data-path collective ("scaling": "weak").
 
-Also reported (rank 0): p50 per-task device latency (hipEvents on the worker
-stream, linear-interpolated percentile as src/core/latency_statistics.hpp:52-93),
-p50 end-to-end latency including pinned H2D + D2H, the dominant kernel's
-roofline (hipEvents on its launch stream), the CPU codelet baseline (oracle =
-ATen CPU forward of the same module, bounded sample) and, single-GPU only,
-extras: plain-fp16 throughput, BERT-base seq128 bs8, ResNet-18 bs1 latency and
-the PCIe-inclusive mini-runtime path.
+Also reported (rank 0, single GPU):
+* `e2e`: the SURVEY 8(d) serving metric -- the mini-runtime (pinned slot pools, H2D/D2H, pipelined
+  workers) driven by the C++ client loop: inf/s = inferences / (last response - first request)
+  (inference_client.cpp:259-270), p50/p95/p99 request latency incl. H2D + D2H
+  (latency_statistics.hpp:52-93);
+* the dominant kernel's roofline, measured under the same four-stream load (hipEvents on its
+  launch stream) and isolated, with HBM traffic and MFMA-busy from the committed rocprofv3 PMC
+  passes (profiles/r02/);
+* the CPU codelet baseline: the C++ LibTorch CPU codelet (libspi_torch.so, the reference's
+  cpu_inference_func restated) on a TorchScript export of the same model, on the host's cores;
+* extras: plain fp16, ResNet-18 bs1, bs1 requests batched by the runtime (adaptive vs fixed),
+  BERT-base seq128 bs8 (C3), ResNet-152 bs32 (C4), ViT-L/16 bs16 (C5).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import glob
 import importlib
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -46,6 +52,7 @@ WORKLOADS = {
 }
 PEAK_TFLOPS = {"fp16": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+PROFILE_ROUND = "r02"
 
 
 def percentile(samples, p):
@@ -126,37 +133,35 @@ class Harness:
         if a.status != self.N.SPI_OK:
             raise RuntimeError(a.error.decode())
 
-    def throughput(self, steps, warmup, world=1, dist=None):
-        """Timed region: `steps` rounds of one task per worker, no instrumentation
-        inside (timing events on every task cost ~25 % of throughput on ROCm).
-        Per-task latency comes from a separate pass of the same load with events."""
-        torch = self.torch
-        W = len(self.calls)
-        for _ in range(warmup):
-            for w in range(W):
+    def rounds(self, n):
+        for _ in range(n):
+            for w in range(len(self.calls)):
                 self.task(w)
+
+    def throughput(self, steps, warmup, tasks_per_step=1, world=1, dist=None):
+        """Timed region: exactly `steps` steps of `tasks_per_step` tasks per worker, no
+        instrumentation inside (timing events on every task cost ~25 % on ROCm)."""
+        torch = self.torch
+        self.rounds(warmup * tasks_per_step)
         torch.cuda.synchronize(self.dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
-        for _ in range(steps):
-            for w in range(W):
-                self.task(w)
+        self.rounds(steps * tasks_per_step)
         torch.cuda.synchronize(self.dev)
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
-        elapsed = reduce_max_elapsed(t1 - t0, world)
-        return elapsed, self.loaded_latency(min(steps, 50))
+        return reduce_max_elapsed(t1 - t0, world)
 
-    def loaded_latency(self, steps):
+    def loaded_latency(self, rounds):
         """Device latency of each task (events on its worker stream) with every worker busy."""
         torch = self.torch
         W = len(self.calls)
         events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(W)]
-                  for _ in range(steps)]
-        for k in range(steps):
+                  for _ in range(rounds)]
+        for k in range(rounds):
             for w in range(W):
                 self.task(w, events[k][w])
         torch.cuda.synchronize(self.dev)
@@ -181,55 +186,70 @@ class Harness:
                 out.append((time.perf_counter() - ts) * 1e3)
         return out
 
-    def dominant_kernel(self, precision, model=""):
-        ops = self.replica.profile(self.d_in[0], self.d_out[0], self.streams[0].cuda_stream)
-        totals = {}
-        for op in ops:
-            t = totals.setdefault(op["name"], [0.0, 0, op["flops"], op["bytes"]])
-            t[0] += op["ms"]
-            t[1] += 1
-        name, (tot, cnt, flops, nbytes) = max(totals.items(), key=lambda kv: kv[1][0])
-        ms = tot / cnt
-        fwd_ms = sum(o["ms"] for o in ops)
-        fwd_flops = sum(o["flops"] for o in ops)
-        peak = PEAK_TFLOPS[precision]
-        traffic, src = measured_traffic(model, self.batch, precision, name)
-        common = {"kernel": name, "launches_per_forward": cnt, "traffic": traffic, "traffic_source": src,
-                  "avg_launch_ms": round(ms, 5), "forward_share": round(tot / fwd_ms, 4),
-                  "forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5)}
-        if flops == 0:  # a byte-moving op dominates: HBM roofline on its algorithmic bytes
-            ach = nbytes / (ms * 1e-3) / 1e9
-            return {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(ach / PEAK_HBM_GBS, 5), "algorithmic_bytes_per_launch": nbytes, **common}
-        ach = flops / (ms * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 5), "algorithmic_flops_per_launch": flops,
-                "mfma_issue_per_flop": 3 if precision == "fp16x3" else 1, **common}
+    def op_profile(self, loaded: bool, repeats: int = 5):
+        """Per-op device time of one forward on worker 0's stream (every launch bracketed by
+        hipEvents on that stream), averaged over `repeats` forwards.  loaded=True: the other
+        workers run back-to-back tasks meanwhile -- the four-stream load `value` is measured under."""
+        torch = self.torch
+        W = len(self.calls)
+        acc = {}
+        for _ in range(repeats):
+            if loaded:
+                for _ in range(12):  # ~12 tasks per busy worker covers the profiled forward
+                    for w in range(1, W):
+                        self.task(w)
+            ops = self.replica.profile(self.d_in[0], self.d_out[0], self.streams[0].cuda_stream)
+            torch.cuda.synchronize(self.dev)
+            for op in ops:
+                a = acc.setdefault(op["name"], [0.0, 0, op["flops"], op["bytes"]])
+                a[0] += op["ms"]
+                a[1] += 1
+        return {k: (v[0] / repeats, v[1] // repeats, v[2], v[3]) for k, v in acc.items()}
 
 
-def measured_traffic(model, batch, precision, op):
-    """HBM bytes per launch of `op` from the committed PMC profile
-    profiles/<round>/traffic_<model>_bs<batch>_<precision>.json (tools/pmc_traffic.sh:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH x2 correction), or None."""
-    import glob
-
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{model}_bs{batch}_{precision}.json")))
+def committed_profile(kind, model, batch, precision):
+    """profiles/<round>/<kind>_<model>_bs<batch>_<precision>.json (rocprofv3 PMC passes, tools/pmc_*.sh)."""
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{kind}_{model}_bs{batch}_{precision}.json")))
     if not hits:
-        return None, None
+        return {}, None
     with open(hits[-1]) as f:
-        ops = json.load(f).get("ops", {})
-    if op not in ops:
-        return None, None
-    return ops[op]["hbm_bytes_per_launch"], os.path.relpath(hits[-1], ROOT)
+        return json.load(f).get("ops", {}), os.path.relpath(hits[-1], ROOT)
 
 
-def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4, req_batch=None, coalesce=1,
-                delay_us=0):
-    """Closed loop through the mini-runtime (host buffers, pinned slots, H2D/D2H):
-    inf/s = inferences / (last response - first request) (inference_client.cpp:259-270).
-    req_batch < batch: requests of req_batch samples, merged by the runtime's dynamic
-    batching into codelet calls of up to `batch` (coalesce jobs, delay_us wait)."""
-    rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
+def roofline(h, precision, model):
+    """The dominant op under the four-stream load (largest device time per forward), its
+    algorithmic FLOPs per launch over its mean launch duration; the same op isolated beside it."""
+    loaded = h.op_profile(True)
+    iso = h.op_profile(False)
+    name, (tot, cnt, flops, nbytes) = max(loaded.items(), key=lambda kv: kv[1][0])
+    ms = tot / max(cnt, 1)
+    ms_iso = iso[name][0] / max(iso[name][1], 1)
+    fwd_ms = sum(v[0] for v in iso.values())
+    fwd_flops = sum(v[2] * v[1] for v in iso.values())
+    peak = PEAK_TFLOPS[precision]
+    traffic, tsrc = committed_profile("traffic", model, h.batch, precision)
+    mfma, msrc = committed_profile("mfma", model, h.batch, precision)
+    common = {"kernel": name, "launches_per_forward": cnt, "avg_launch_ms": round(ms, 5),
+              "avg_launch_ms_isolated": round(ms_iso, 5),
+              "forward_share_loaded": round(tot / sum(v[0] for v in loaded.values()), 4),
+              "traffic": traffic.get(name, {}).get("hbm_bytes_per_launch"), "traffic_source": tsrc,
+              "mfma_busy_pct": mfma.get(name, {}).get("mfma_busy_pct"), "mfma_source": msrc,
+              "isolated_forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5),
+              "measured": "hipEvents on the launch stream, 5 forwards under the 4-stream load / isolated"}
+    if flops == 0:
+        ach = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach / PEAK_HBM_GBS, 5), "algorithmic_bytes_per_launch": nbytes,
+                "frac_isolated": round(nbytes / (ms_iso * 1e-3) / 1e9 / PEAK_HBM_GBS, 5), **common}
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 5),
+            "frac_isolated": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 5),
+            "algorithmic_flops_per_launch": flops, "mfma_issue_per_flop": 3 if precision == "fp16x3" else 1,
+            **common}
+
+
+def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None, workers=4, schedule=None, **kw):
+    """The serving path: mini-runtime (pinned slots, H2D/D2H, pipelined workers) + C++ client loop."""
     rb = req_batch or batch
     host_inputs, out_shape = make_inputs(name, rb, np.random.default_rng(7))
     if name.startswith("bert"):
@@ -238,53 +258,112 @@ def runtime_e2e(spi, replica, name, batch, inflight=8, requests=160, workers=4, 
         in_specs = [((3, 224, 224), np.float32)]
     out_elems = int(np.prod(out_shape[1:]))
     rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers,
-                       coalesce_max_jobs=coalesce, coalesce_delay_us=delay_us)
-    outs = [np.empty(out_shape, np.float32) for _ in range(inflight)]
-    submitted = 0
-    t0 = time.perf_counter()
-    while submitted < requests:
-        done = len(rt.completions)
-        while submitted < requests and submitted - done < inflight:
-            rt.submit(submitted, host_inputs, [outs[submitted % inflight]])
-            submitted += 1
-        time.sleep(0.0002)
-    rt.drain()
-    first = min(c.submit_ns for c in rt.completions)
-    last = max(c.complete_ns for c in rt.completions)
-    lat = [c.latency_ms for c in rt.completions]
-    ok, failed = rt.stats()
-    jobs_per_call = float(np.mean([c.task_jobs for c in rt.completions]))
+                       **kw)
+    r = rt.loadgen(host_inputs, requests=requests, inflight=inflight, warmup=4 * workers * 2, schedule=schedule)
+    target = rt.batch_target
     rt.close()
-    return {"value": round(requests * rb / ((last - first) * 1e-9), 2), "unit": "inferences/s",
-            "p50_latency_ms": round(percentile(lat, 50), 4), "p95_latency_ms": round(percentile(lat, 95), 4),
-            "requests": requests, "request_batch": rb, "max_batch": batch, "inflight": inflight,
-            "workers": workers, "coalesce_max_jobs": coalesce, "coalesce_delay_us": delay_us,
-            "mean_jobs_per_codelet_call": round(jobs_per_call, 2), "failed": failed,
-            "wall_s": round(time.perf_counter() - t0, 3)}
+    out = {"value": round(r["inferences_per_s"], 2), "unit": "inferences/s", "p50_latency_ms": round(r["p50_ms"], 4),
+           "p95_latency_ms": round(r["p95_ms"], 4), "p99_latency_ms": round(r["p99_ms"], 4),
+           "requests": r["completed"], "request_batch": rb, "max_batch": batch, "inflight": inflight,
+           "workers": workers, "mean_task_batch": round(r["mean_task_batch"], 2),
+           "p50_queue_ms": round(r["p50_queue_ms"], 4), "failed": r["failed"], "rejected": r["rejected"],
+           "seconds": round(r["seconds"], 3)}
+    if r["error"]:
+        out["first_error"] = r["error"]
+    if kw.get("batching") is not None:
+        out["final_batch_target"] = target
+    return out
+
+
+def host_cores():
+    nodes = glob.glob("/sys/devices/system/node/node[0-9]*")
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "numa_nodes": max(1, len(nodes)),
+            "threads_used": min(share, affinity)}
+
+
+def cpu_baseline(model, name, batch, seconds):
+    """The C++ LibTorch CPU codelet (spi_cpu_inference_func + spi_torch_cpu_forward) on a TorchScript
+    export of the same model: layout (i) one worker with all the host threads as intra-op threads
+    (group_cpu_by_numa, starpu_setup.cpp:299-385), layout (ii) one worker per NUMA node."""
+    import torch
+
+    lt = importlib.import_module("starpu-inference-server_amd.libtorch")
+    cores = host_cores()
+    n = cores["threads_used"]
+    numa = cores["numa_nodes"]
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, f"{name}.pt")
+        torch.jit.trace(model, torch.rand(1, 3, 224, 224)).save(path)
+        ts = lt.TorchScriptModule(path)
+    rng = np.random.default_rng(0)
+    x8 = rng.random((batch, 3, 224, 224), dtype=np.float32)
+    x1 = x8[:1].copy()
+    # warm-up, then ~seconds of CPU work per configuration
+    ts.bench([x1], [4000], workers=1, threads=n, seconds=0.5)
+    main = ts.bench([x8], [batch * 4000], workers=1, threads=n, seconds=seconds)
+    c1 = ts.bench([x1], [4000], workers=1, threads=n, seconds=seconds / 2)
+    per = max(1, n // numa)
+    c1_numa = ts.bench([x1], [4000], workers=numa, threads=per, seconds=seconds / 2)
+    ts.close()
+    return {
+        "value": round(main["inferences_per_s"], 3), "unit": "inferences/s", "cores": n, "kind": "port",
+        "sample": f"{main['tasks']} CPU-codelet tasks ({name} bs{batch} fp32, TorchScript, libspi_torch.so: "
+                  f"InferenceMode forward + copy_output_to_buffer behind spi_cpu_inference_func), "
+                  f"{main['seconds']:.1f} s, 1 worker x {n} intra-op threads",
+        "p50_ms": round(main["p50_ms"], 3), "host": cores,
+        "c1_resnet18_bs1_fp32": {
+            "layout_i_one_worker_all_threads": {"value": round(c1["inferences_per_s"], 3), "unit": "inferences/s",
+                                                "p50_ms": round(c1["p50_ms"], 3), "workers": 1, "threads": n,
+                                                "tasks": c1["tasks"]},
+            "layout_ii_worker_per_numa_node": {"value": round(c1_numa["inferences_per_s"], 3),
+                                               "unit": "inferences/s", "p50_ms": round(c1_numa["p50_ms"], 3),
+                                               "workers": numa, "threads_per_worker": per,
+                                               "tasks": c1_numa["tasks"]}} if name == "resnet18" else None,
+    }
+
+
+def config_line(spi, zoo, name, batch, precision, workers, streams, steps, dev, seq=128):
+    """Device-resident inf/s, loaded p50 task latency and roofline for one BASELINE config."""
+    model = zoo.build(name, seed=0)
+    rep = spi.ModelReplica(model, dev, precision, max_batch=batch, seq_len=seq if name.startswith("bert") else 0,
+                           graphs=True)
+    h = Harness(spi, rep, name, dev, batch, workers, np.random.default_rng(3), streams)
+    el = h.throughput(steps, 2, 1)
+    lat = h.loaded_latency(10)
+    out = {"value": round(workers * batch * steps / el, 2), "unit": "sequences/s" if name.startswith("bert") else
+           "inferences/s", "dtype": precision, "batch": batch,
+           "p50_task_latency_ms": round(percentile(lat, 50), 4),
+           "gflop_per_inference": round(rep.flops(1) / 1e9, 3), "roofline": roofline(h, precision, name)}
+    out["model_tflops"] = round(rep.flops(1) * out["value"] / 1e12, 2)
+    return out, rep, model
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet18", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--precision", default="fp16x3", choices=["fp16", "fp16x3", "fp32"])
     ap.add_argument("--workers", type=int, default=4, help="worker streams per GPU")
+    ap.add_argument("--tasks-per-step", type=int, default=8, help="codelet calls per worker per step")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--latency-iters", type=int, default=40)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline budget per layout (0 = skip)")
+    ap.add_argument("--e2e-requests", type=int, default=4000)
     ap.add_argument("--extras", type=int, default=1, help="single-GPU extra measurements (0 = skip)")
     args = ap.parse_args()
-    # One HIP hardware queue per worker stream: HIP maps streams onto
-    # GPU_MAX_HW_QUEUES queues round-robin (default 4, shared with torch's own
-    # streams), and worker streams that share a queue run serially -- measured
-    # 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues (16 measured
-    # the same as 8).  Room for two sets of worker streams: the harness's and the
-    # mini-runtime extra's own.  Must be set before the first HIP call (DESIGN.md,
-    # INTEGRATION.md).
-    queues = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 2 * args.workers + 4))
+    # One HIP hardware queue per stream: HIP maps streams onto GPU_MAX_HW_QUEUES queues
+    # round-robin (default 4, shared with torch's own streams), and streams that share a queue
+    # run serially -- 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues.  Room for the
+    # harness's worker streams plus the runtime's workers and copy stream.  Must be set before the
+    # first HIP call (DESIGN.md 1).
+    queues = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 2 * args.workers + 8))
     os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -296,6 +375,7 @@ def main():
 
     spi = importlib.import_module("starpu-inference-server_amd")
     zoo = importlib.import_module("starpu-inference-server_amd.zoo")
+    rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -309,8 +389,10 @@ def main():
     replica = spi.ModelReplica(model, dev, args.precision, max_batch=args.batch,
                                seq_len=seq if args.model.startswith("bert") else 0, graphs=bool(args.graphs))
     h = Harness(spi, replica, args.model, dev, args.batch, args.workers, np.random.default_rng(rank))
-    elapsed, task_lat = h.throughput(args.steps, args.warmup, world, dist)
-    value = world * args.workers * args.batch * args.steps / elapsed
+    elapsed = h.throughput(args.steps, args.warmup, args.tasks_per_step, world, dist)
+    per_step = args.workers * args.tasks_per_step * args.batch
+    value = world * per_step * args.steps / elapsed
+    task_lat = h.loaded_latency(20)
 
     result = {
         "metric": BASELINE_METRIC,
@@ -330,9 +412,11 @@ def main():
             "workload": WORKLOADS[args.model],
             "batch_per_task": args.batch,
             "workers_per_gpu": args.workers,
-            "tasks_per_step_per_gpu": args.workers,
+            "step": f"{args.tasks_per_step} codelet calls on each of the {args.workers} worker streams "
+                    f"({per_step} inferences per GPU)",
             "precision_mode": {"fp16x3": "split-fp16 MFMA (hi/lo fp16 operands, fp32 accumulate): fp32-grade parity",
                                "fp16": "fp16 MFMA operands, fp32 accumulate", "fp32": "fp32 MFMA"}[args.precision],
+            "inputs": "resident in HBM (device-resident codelet rate; the PCIe-inclusive serving rate is `e2e`)",
             "graphs": bool(args.graphs),
             "hip_hw_queues": queues,
             "parallelism": f"replicas x{world} (request sharding, no collective)",
@@ -341,79 +425,69 @@ def main():
         "p95_task_latency_ms": round(percentile(task_lat, 95), 4),
     }
     if rank == 0:
-        e2e = h.serial_e2e(args.latency_iters)
-        result["p50_e2e_latency_ms_incl_h2d_d2h"] = round(percentile(e2e, 50), 4)
-        result["e2e_inferences_per_s_serial"] = round(args.batch / (percentile(e2e, 50) * 1e-3), 2)
         result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
         result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
-        result["roofline"] = h.dominant_kernel(args.precision, args.model)
+        result["roofline"] = roofline(h, args.precision, args.model)
+    if rank == 0 and world == 1:
+        # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
+        e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=4 * args.workers,
+                          workers=args.workers)
+        e2e["fraction_of_device_resident"] = round(e2e["value"] / value, 4)
+        e2e["pipeline"] = "4 workers x depth 2, per-device copy stream, pinned slot pool of 8, 4 host copy threads"
+        result["e2e"] = e2e
+        e2e1 = h.serial_e2e(40)
+        result["p50_serial_e2e_latency_ms"] = round(percentile(e2e1, 50), 4)
 
-    if rank == 0 and args.cpu_seconds > 0:
-        from oracle.cpu_codelet import cpu_inference
-
-        cores = torch.get_num_threads()
-
-        def cpu_sample(inputs, seconds, cap):
-            cpu_inference(model, inputs)  # warm-up
-            times = []
-            while sum(times) < seconds and len(times) < cap:
-                ts = time.perf_counter()
-                cpu_inference(model, inputs)
-                times.append(time.perf_counter() - ts)
-            return times
-
-        times = cpu_sample(h.host_inputs, args.cpu_seconds, 200)
-        t_cpu = sum(times)
-        result["cpu_baseline"] = {
-            "value": round(len(times) * args.batch / t_cpu, 3), "unit": "inferences/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{len(times)} forwards of the same {args.model} batch {args.batch} fp32 on host ATen "
-                      f"(torch {torch.__version__}, {cores} intra-op threads), {t_cpu:.1f}s",
-            "p50_ms": round(percentile([t * 1e3 for t in times], 50), 3)}
-        if args.model == "resnet18":
-            # BASELINE configs[0] (C1): the CPU codelet alone, ResNet-18 bs=1 fp32
-            one = [x[:1] for x in h.host_inputs]
-            t1 = cpu_sample(one, min(4.0, args.cpu_seconds), 400)
-            result["cpu_baseline"]["c1_resnet18_bs1_fp32"] = {
-                "value": round(len(t1) / sum(t1), 3), "unit": "inferences/s",
-                "p50_ms": round(percentile([t * 1e3 for t in t1], 50), 3), "forwards": len(t1)}
+    if rank == 0 and args.cpu_seconds > 0 and args.model == "resnet18":
+        result["cpu_baseline"] = cpu_baseline(model, args.model, args.batch, args.cpu_seconds)
 
     if rank == 0 and world == 1 and args.extras and args.model == "resnet18":
         extras = {}
-        # plain fp16 operands on the same workload (faster, 1.8e-3 parity on this network)
+        # plain fp16 operands on the same workload (faster; 1.0e-3 .. 2.4e-3 parity on these networks)
         r16 = spi.ModelReplica(model, dev, "fp16", max_batch=args.batch, graphs=True)
         h16 = Harness(spi, r16, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
-        el, lat = h16.throughput(args.steps, args.warmup)
+        el = h16.throughput(args.steps, 2, args.tasks_per_step)
         extras["resnet18_bs8_fp16_plain"] = {
-            "value": round(args.workers * args.batch * args.steps / el, 2), "unit": "inferences/s",
-            "p50_task_latency_ms": round(percentile(lat, 50), 4), "parity_normalised_max_err": 1.8e-3}
-        # ResNet-18 bs=1 latency (the metric names it)
+            "value": round(per_step * args.steps / el, 2), "unit": "inferences/s",
+            "parity_normalised_max_err": 1.0e-3, "note": "not parity-grade on ResNet: never the C2 figure"}
+        del r16, h16
+        # ResNet-18 bs=1 (the metric names it): device-resident tasks, and bs1 requests served
         r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
         h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2), h.streams)
-        el, lat = h1.throughput(args.steps, args.warmup)
-        e2e1 = h1.serial_e2e(args.latency_iters)
-        extras["resnet18_bs1"] = {"value": round(args.workers * args.steps / el, 2), "unit": "inferences/s",
-                                  "p50_task_latency_ms": round(percentile(lat, 50), 4),
-                                  "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2e1, 50), 4),
-                                  "dtype": args.precision}
-        # the PCIe-inclusive serving path through the mini-runtime (never `value`)
-        extras["resnet18_bs8_runtime_pcie"] = runtime_e2e(spi, replica, "resnet18", args.batch)
-        # bs=1 client requests, dynamically batched by the runtime into calls of <= 8
-        extras["resnet18_bs1_requests_batched8_runtime_pcie"] = runtime_e2e(
-            spi, replica, "resnet18", args.batch, inflight=64, requests=1280, req_batch=1, coalesce=args.batch,
-            delay_us=500)
-        del r16, h16, r1, h1
-        # BERT-base seq128 bs8 fp16 (BASELINE configs[2])
-        bmodel = zoo.build("bert_base", seed=0)
-        rb = spi.ModelReplica(bmodel, dev, "fp16", max_batch=8, seq_len=seq, graphs=True)
-        hb = Harness(spi, rb, "bert_base", dev, 8, args.workers, np.random.default_rng(3), h.streams)
-        el, lat = hb.throughput(max(20, args.steps // 4), 5)
-        e2eb = hb.serial_e2e(10)
-        extras["bert_base_seq128_bs8_fp16"] = {
-            "value": round(args.workers * 8 * max(20, args.steps // 4) / el, 2), "unit": "sequences/s",
-            "p50_task_latency_ms": round(percentile(lat, 50), 4),
-            "p50_e2e_latency_ms_incl_h2d_d2h": round(percentile(e2eb, 50), 4),
-            "gflop_per_seq": round(rb.flops(1) / 1e9, 3), "roofline": hb.dominant_kernel("fp16", "bert_base")}
+        el = h1.throughput(args.steps, 2, args.tasks_per_step)
+        lat1 = h1.loaded_latency(20)
+        ser1 = h1.serial_e2e(40)
+        extras["resnet18_bs1_tasks"] = {
+            "value": round(args.workers * args.tasks_per_step * args.steps / el, 2), "unit": "inferences/s",
+            "p50_task_latency_ms": round(percentile(lat1, 50), 4),
+            "p50_serial_e2e_latency_ms": round(percentile(ser1, 50), 4), "dtype": args.precision}
+        del r1, h1
+        # bs1 client requests batched server-side into codelet calls of <= 8: closed loop, and the
+        # bursty open-loop schedule shaped like ci/perf/ci_perf_resnet.csv (delta_us x repeat, time
+        # scaled by 1/10 for this GPU), fixed coalescer vs adaptive strategy
+        extras["resnet18_bs1_requests_closed_loop_adaptive"] = runtime_e2e(
+            rtmod, replica, "resnet18", args.batch, 6000, inflight=64, req_batch=1,
+            batching=rtmod.batching_config("adaptive", 1, args.batch, coalesce_timeout_us=200, congestion=True,
+                                           tick_us=500, entry_horizon_us=3000, exit_horizon_us=7000))
+        sched = [(170, 3000), (30, 300), (300, 3000)]
+        for label, kw in [("fixed", dict(coalesce_max_jobs=args.batch, coalesce_delay_us=500)),
+                          ("adaptive", dict(batching=rtmod.batching_config(
+                              "adaptive", 1, args.batch, coalesce_timeout_us=500, congestion=True, tick_us=500,
+                              entry_horizon_us=3000, exit_horizon_us=7000)))]:
+            extras[f"resnet18_bs1_requests_bursty_schedule_{label}"] = runtime_e2e(
+                rtmod, replica, "resnet18", args.batch, 0, inflight=256, req_batch=1, max_queue=256,
+                schedule=sched, **kw)
+            extras[f"resnet18_bs1_requests_bursty_schedule_{label}"]["schedule_delta_us_repeat"] = sched
+        # C3 BERT-base seq128 bs8 fp16; C4 ResNet-152 bs32 fp16x3; C5 ViT-L/16 bs16 fp16 (single GPU)
+        for key, name, b, prec in [("c3_bert_base_seq128_bs8_fp16", "bert_base", 8, "fp16"),
+                                   ("c4_resnet152_bs32_fp16x3", "resnet152", 32, "fp16x3"),
+                                   ("c5_vit_l_16_bs16_fp16", "vit_l_16", 16, "fp16")]:
+            line, rep, mdl = config_line(spi, zoo, name, b, prec, args.workers, h.streams, max(10, args.steps // 2),
+                                         dev)
+            line["e2e"] = runtime_e2e(rtmod, rep, name, b, 400 if name != "bert_base" else 1000,
+                                      inflight=4 * args.workers, workers=args.workers)
+            extras[key] = line
+            del rep, mdl
         result["extras"] = extras
 
     if world > 1:

@@ -284,6 +284,12 @@ int spi_model_profile(spi_model* model, void* stream, int64_t batch, int64_t seq
                       int32_t max_ops);
 /* Capture launch-bound forwards into hipGraphs (per stream, per batch). */
 void spi_model_set_graphs(spi_model* model, int32_t enable);
+/* Per-worker warm-up (inference_runner.cpp:507-560): allocate `stream`'s
+ * workspace and, with graphs on, capture the forward body for (batch, seq,
+ * with_mask) now rather than inside a live request.  Enqueues no work.
+ * seq / with_mask matter for BERT only.  Returns SPI_OK or an error status
+ * (message in spi_last_error()). */
+int spi_model_warmup(spi_model* model, void* stream, int64_t batch, int64_t seq, int32_t with_mask);
 
 /* ---------------------------------------------------------------------------
  * Small device utilities so hosts without a HIP runtime binding (ctypes,

@@ -177,6 +177,7 @@ _PROTOS = {
     "spi_model_flops": (C.c_double, [C.c_void_p, C.c_int64]),
     "spi_model_describe": (C.c_char_p, [C.c_void_p]),
     "spi_model_set_graphs": (None, [C.c_void_p, C.c_int32]),
+    "spi_model_warmup": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32]),
     "spi_model_profile": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_void_p), C.POINTER(C.c_float), C.POINTER(C.c_double),
                                     C.POINTER(C.c_double), C.c_char_p, C.c_int32, C.c_int32]),

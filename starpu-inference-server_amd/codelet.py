@@ -195,6 +195,11 @@ class ModelReplica:
     def set_graphs(self, on: bool) -> None:
         lib.spi_model_set_graphs(self.handle, 1 if on else 0)
 
+    def warmup(self, stream: int, batch: int, seq: int = 0, with_mask: bool = True) -> None:
+        """Allocate `stream`'s workspace and pre-capture its (batch, seq) graph (per-worker warm-up)."""
+        if lib.spi_model_warmup(self.handle, C.c_void_p(stream), batch, seq, int(with_mask)) != N.SPI_OK:
+            raise InferenceExecutionException(f"warmup failed: {N.last_error()}")
+
     @property
     def description(self) -> str:
         return lib.spi_model_describe(self.handle).decode()

@@ -393,6 +393,19 @@ void spi_model_set_graphs(spi_model* m, int32_t on) {
   if (m) m->impl->set_graphs(on != 0);
 }
 
+int spi_model_warmup(spi_model* m, void* stream, int64_t batch, int64_t seq, int32_t with_mask) {
+  if (!m) return SPI_ERR_INVALID_ARGUMENT;
+  try {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != m->impl->device()) (void)hipSetDevice(m->impl->device());
+    m->impl->warmup(static_cast<hipStream_t>(stream), (int)batch, (int)seq, with_mask != 0);
+    return SPI_OK;
+  } catch (const std::exception& e) {
+    tl_last_error = e.what();
+    return SPI_ERR_DEVICE;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Device utilities
 // ---------------------------------------------------------------------------

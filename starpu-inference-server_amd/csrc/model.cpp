@@ -55,6 +55,12 @@ int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 constexpr size_t kCounterSlots = 16384;  // >= tiles of any split GEMM (checked per launch)
 
+// Graph capture vs allocation: a hipMalloc on one worker thread while another
+// thread's stream is capturing invalidates that capture ("operation failed due
+// to a previous error during capture").  Workspace allocation and graph capture
+// therefore never overlap, process-wide (all replicas, all worker threads).
+std::mutex g_capture_mu;
+
 // ---------------------------------------------------------------------------
 // Workspace: activation buffers for one stream at max_batch.
 // ---------------------------------------------------------------------------
@@ -664,6 +670,7 @@ Workspace* Model::workspace(hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = ws_.find(s);
   if (it != ws_.end()) return it->second.get();
+  std::lock_guard<std::mutex> cap(g_capture_mu);
   auto w = std::make_unique<Workspace>();
   const size_t es = f16_ ? 2 : 4;
   const int B = max_batch_;
@@ -738,7 +745,9 @@ Workspace* Model::workspace(hipStream_t s) {
   w->partial_floats = partial;
   SPI_HIP(hipMalloc(&w->partial, partial * sizeof(float)));
   SPI_HIP(hipMalloc(&w->counters, kCounterSlots * sizeof(int)));
-  SPI_HIP(hipMemset(w->counters, 0, kCounterSlots * sizeof(int)));
+  // stream-ordered zeroing (a synchronous null-stream memset would also break
+  // concurrent captures); it precedes every use of the tickets on this stream
+  SPI_HIP(hipMemsetAsync(w->counters, 0, kCounterSlots * sizeof(int), s));
   Workspace* raw = w.get();
   ws_[s] = std::move(w);
   return raw;
@@ -908,34 +917,56 @@ void Model::forward(hipStream_t s, int B, int S, size_t n, const void* const* in
     affine(static_cast<const float*>(in[0]), static_cast<float*>(out[0]), n, aff_scale_, aff_shift_, s);
     return;
   }
+  if (family_ != SPI_FAMILY_BERT) S = 0;  // only BERT's graphs depend on the sequence length
   Workspace* w = workspace(s);
   prologue(*w, B, S, in, s);
   if (graphs_ && s != nullptr) {
-    const int key = (B * 2 + (w->has_mask ? 1 : 0)) * 4096 + S;
-    auto it = w->graphs.find(key);
-    if (it == w->graphs.end()) {
-      SPI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      hipGraph_t g = nullptr;
-      try {
-        body(*w, B, S, s);
-      } catch (...) {
-        // Leave the worker stream usable: end the capture before rethrowing,
-        // otherwise every later task on this stream fails.
-        if (hipStreamEndCapture(s, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
-        (void)hipGetLastError();
-        throw;
-      }
-      SPI_HIP(hipStreamEndCapture(s, &g));
-      hipGraphExec_t e = nullptr;
-      SPI_HIP(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
-      (void)hipGraphDestroy(g);
-      it = w->graphs.emplace(key, e).first;
-    }
-    SPI_HIP(hipGraphLaunch(it->second, s));
+    SPI_HIP(hipGraphLaunch(graph(*w, B, S, s), s));
   } else {
     body(*w, B, S, s);
   }
   epilogue(*w, B, S, out, s);
+}
+
+// The captured body for (batch, mask, S) on this stream's workspace, captured
+// on first use (or ahead of time by warmup()).
+hipGraphExec_t Model::graph(Workspace& w, int B, int S, hipStream_t s) {
+  const int key = (B * 2 + (w.has_mask ? 1 : 0)) * 4096 + S;
+  auto it = w.graphs.find(key);
+  if (it != w.graphs.end()) return it->second;
+  std::lock_guard<std::mutex> cap(g_capture_mu);
+  SPI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  hipGraph_t g = nullptr;
+  try {
+    body(w, B, S, s);
+  } catch (...) {
+    // Leave the worker stream usable: end the capture before rethrowing,
+    // otherwise every later task on this stream fails.
+    if (hipStreamEndCapture(s, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    throw;
+  }
+  SPI_HIP(hipStreamEndCapture(s, &g));
+  hipGraphExec_t e = nullptr;
+  const hipError_t ie = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  SPI_HIP(ie);
+  return w.graphs.emplace(key, e).first->second;
+}
+
+// Per-worker warm-up (the reference warms each worker up before serving,
+// inference_runner.cpp:507-560): allocate this stream's workspace and capture
+// the body graph for (batch, S, mask) now, so no capture or allocation lands on
+// a live request.  Runs nothing on the device.
+void Model::warmup(hipStream_t s, int B, int S, bool mask) {
+  if (device_ < 0) throw std::runtime_error("host-only replica (device < 0) cannot run a forward");
+  if (family_ == SPI_FAMILY_AFFINE) return;
+  if (B < 1 || B > max_batch_) throw std::runtime_error("warmup batch exceeds replica max_batch");
+  if (family_ == SPI_FAMILY_BERT && (S < 1 || S > seq_)) throw std::runtime_error("warmup sequence length out of range");
+  Workspace* w = workspace(s);
+  if (!graphs_ || s == nullptr) return;
+  w->has_mask = family_ == SPI_FAMILY_BERT && mask;
+  (void)graph(*w, B, family_ == SPI_FAMILY_BERT ? S : 0, s);
 }
 
 }  // namespace spi

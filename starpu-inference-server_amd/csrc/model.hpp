@@ -72,6 +72,8 @@ class Model {
   // Enqueue the forward on `s`; never synchronises.
   // S: BERT sequence length (ignored otherwise); n: AFFINE element count.
   void forward(hipStream_t s, int batch, int S, size_t n, const void* const* in, void* const* out);
+  // Allocate the stream's workspace and capture its (batch, S, mask) graph ahead of serving.
+  void warmup(hipStream_t s, int batch, int S, bool mask);
 
   // Per-op profile of one forward: each launch bracketed by hipEvents on `s`.
   struct OpRecord {
@@ -93,6 +95,7 @@ class Model {
   void build_bert(const std::map<std::string, const spi_named_tensor*>& p);
   void build_vit(const std::map<std::string, const spi_named_tensor*>& p);
   Workspace* workspace(hipStream_t s);
+  hipGraphExec_t graph(Workspace& w, int batch, int S, hipStream_t s);
   void body(Workspace& w, int batch, int S, hipStream_t s);
   void prologue(Workspace& w, int batch, int S, const void* const* in, hipStream_t s);
   void epilogue(Workspace& w, int batch, int S, void* const* out, hipStream_t s);

@@ -731,6 +731,14 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       if (!wok) return cleanup_fail("stream creation failed for worker " + std::to_string(wid - 1));
     }
   }
+  // per-worker warm-up before serving: workspaces + graphs for max_batch
+  const int64_t seq = cfg.input_ndims[0] >= 1 ? cfg.input_dims[0][0] : 0;
+  for (auto& w : rt->workers) {
+    (void)hipSetDevice(w->device);
+    if (spi_model_warmup(w->model, w->stream, cfg.max_batch, seq, cfg.num_inputs >= 2) != SPI_OK)
+      return cleanup_fail(std::string("warm-up failed for worker ") + std::to_string(w->worker_id) + ": " +
+                          spi_last_error());
+  }
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
   rt->last_target = cfg.max_batch;
   for (auto& w : rt->workers) w->thread = std::thread(&spi_runtime::run, rt.get(), w.get());

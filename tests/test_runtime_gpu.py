@@ -259,3 +259,47 @@ def test_runtime_loadgen_closed_and_open_loop(spi, zoo, rtmod):
     r = rt.loadgen([x], schedule=[(300, 50), (50, 100), (500, 20)])
     assert r["completed"] + r["rejected"] == 170 and r["failed"] == 0
     rt.close()
+
+
+def test_runtime_concurrent_graph_captures(spi, zoo, rtmod):
+    """Graphs on, ragged batches across 4 workers: every new batch size is captured lazily on
+    its worker thread while the other workers serve -- captures must not break each other
+    (workspace allocation and capture are serialised; counters zeroed stream-ordered)."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=8, image_size=64, graphs=True)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=4)
+    rng = np.random.default_rng(14)
+    jobs = []
+    for rid in range(96):
+        b = 1 + (rid * 5) % 8
+        x = rng.random((b, 3, 64, 64), dtype=np.float32)
+        y = np.full((b, 1000), np.nan, dtype=np.float32)
+        rt.submit(rid, [x], [y])
+        jobs.append((x, y))
+    rt.drain()
+    bad = [c.error for c in rt.completions if c.status != 0]
+    assert not bad, bad[:3]
+    for x, y in jobs:
+        assert normalized_max_error(y, cpu_inference(m, [x])[0]) < 1e-5
+    rt.close()
+
+
+def test_replica_warmup_precaptures(spi, zoo, gpu):
+    """spi_model_warmup: workspace + graph for (batch, seq) ready before the first task; the
+    first task then gives the same bytes as an eager forward."""
+    import torch
+    m = zoo.bert(layers=2, init_std=0.05)
+    rep = spi.ModelReplica(m, 0, "fp16", max_batch=2, seq_len=64, graphs=True)
+    s = torch.cuda.Stream()
+    rep.warmup(s.cuda_stream, 2, 48, True)
+    with pytest.raises(spi.InferenceExecutionException, match="exceeds replica max_batch"):
+        rep.warmup(s.cuda_stream, 3, 48, True)
+    rng = np.random.default_rng(15)
+    ids = torch.from_numpy(rng.integers(0, 30522, (2, 48), dtype=np.int64)).cuda()
+    mask = torch.ones((2, 48), dtype=torch.int64, device="cuda")
+    out_g = torch.empty((2, 48, 768), device="cuda")
+    spi.run_hip(rep, [ids, mask], out_g, stream=s.cuda_stream)
+    rep.set_graphs(False)
+    out_e = torch.empty_like(out_g)
+    spi.run_hip(rep, [ids, mask], out_e, stream=s.cuda_stream)
+    assert torch.equal(out_g, out_e)

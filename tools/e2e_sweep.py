@@ -31,6 +31,12 @@ def main():
     m = zoo.build(args.model, seed=0)
     rep = spi.ModelReplica(m, 0, args.precision, max_batch=args.batch, graphs=True)
     x = np.random.default_rng(0).random((args.batch, 3, 224, 224), dtype=np.float32)
+    import bench
+    h = bench.Harness(spi, rep, args.model, 0, args.batch, 4, np.random.default_rng(1))
+    el, _ = h.throughput(200, 10)
+    print(json.dumps({"device_resident_inf_per_s": round(4 * args.batch * 200 / el, 1),
+                      "queues": os.environ["GPU_MAX_HW_QUEUES"]}), flush=True)
+    del h
     grid = []
     for h2d in ["device_stream", "worker_stream", "worker_copy"]:
         for depth in [1, 2, 3]:
