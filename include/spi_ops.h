@@ -53,6 +53,12 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
                   int32_t stride, int32_t pad, const float* bias, const void* residual,
                   void* y, int32_t act, void* workspace, void* stream);
 
+/* Fused global average pool + linear layer (ResNet avgpool + fc in one launch):
+ * x [B][HW][C] (fp32 / fp16 / split by precision, HW <= 64), W packed from the
+ * [N][C] fc weight; y fp32 [B][N] = act(mean_hw(x) . W^T + bias). */
+int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, int32_t C, const void* W_packed,
+                      int32_t N, const float* bias, float* y, int32_t act, void* workspace, void* stream);
+
 /* Multi-head attention over packed qkv [B*S][3*D] (fp16 or fp32), head_dim 64. */
 int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias, void* ctx,
                      int32_t B, int32_t S, int32_t heads, float scale, void* stream);

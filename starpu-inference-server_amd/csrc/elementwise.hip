@@ -262,6 +262,62 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
                  yt ? yt + (size_t)row * ldy : nullptr, lane);
 }
 
+// LayerNorm rows of D = NV * 256: one wave per row, every lane holds NV float4
+// column groups (c = 4 * (64 j + lane)), so the row moves as 16-byte loads and
+// stores (fp16 copies as 8-byte stores) -- a quarter of the scalar kernel's
+// memory instructions; same two-pass fp32 statistics.
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restrict__ x, int ldx,
+                                                            const float* __restrict__ g,
+                                                            const float* __restrict__ b, float* yf, T* yt,
+                                                            int ldy, int rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = NV * 256;
+  const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * ldx);
+  float4 v[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = xr[j * 64 + lane];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float a0 = v[j].x - mean, a1 = v[j].y - mean, a2 = v[j].z - mean, a3 = v[j].w - mean;
+    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c4 = j * 64 + lane;
+    const float4 gg = g4[c4], bb = b4[c4];
+    float4 o;
+    o.x = (v[j].x - mean) * rstd * gg.x + bb.x;
+    o.y = (v[j].y - mean) * rstd * gg.y + bb.y;
+    o.z = (v[j].z - mean) * rstd * gg.z + bb.z;
+    o.w = (v[j].w - mean) * rstd * gg.w + bb.w;
+    if (yf) reinterpret_cast<float4*>(yf + (size_t)row * ldy)[c4] = o;
+    if (yt) {
+      if constexpr (sizeof(T) == 2) {
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        half4 h;
+        h[0] = static_cast<_Float16>(o.x);
+        h[1] = static_cast<_Float16>(o.y);
+        h[2] = static_cast<_Float16>(o.z);
+        h[3] = static_cast<_Float16>(o.w);
+        reinterpret_cast<half4*>(yt + (size_t)row * ldy)[c4] = h;
+      } else {
+        reinterpret_cast<float4*>(yt + (size_t)row * ldy)[c4] = o;
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bert_embed_kernel(
     const int64_t* ids, const float* word, const float* pos, const float* type0,
@@ -392,6 +448,24 @@ void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStr
 void layernorm(const float* x, int ldx, const float* g, const float* b, float* yf, void* yt,
                int ldy, int rows, int D, float eps, bool f16, hipStream_t s) {
   const dim3 grid((rows + 3) / 4);
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool vec = D % 256 == 0 && (D == 768 || D == 1024) && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) &&
+                   al16(g) && al16(b) && (!yf || al16(yf)) && (!yt || ((reinterpret_cast<uintptr_t>(yt) & 7) == 0));
+  if (vec) {
+    if (D == 768 && f16)
+      hipLaunchKernelGGL((layernorm_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+                         (_Float16*)yt, ldy, rows, eps);
+    else if (D == 768)
+      hipLaunchKernelGGL((layernorm_vec_kernel<float, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
+                         ldy, rows, eps);
+    else if (f16)
+      hipLaunchKernelGGL((layernorm_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+                         (_Float16*)yt, ldy, rows, eps);
+    else
+      hipLaunchKernelGGL((layernorm_vec_kernel<float, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
+                         ldy, rows, eps);
+    return;
+  }
   if (f16)
     hipLaunchKernelGGL((layernorm_kernel<_Float16>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
                        (_Float16*)yt, ldy, rows, D, eps);

@@ -296,6 +296,12 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   const int n0 = tn * BN;
   // m_lim: first row past this tile's valid rows (halo bands end at the image)
   int m0 = tm * BM, m_lim = d.M, h_img = 0, h_oy0 = 0;
+  if constexpr (!HALO) {
+    if (d.pool_rows) {  // fused avgpool + FC: tile row tm = image tm's pixels
+      m0 = tm * d.pool_rows;
+      m_lim = m0 + d.pool_rows;
+    }
+  }
   if constexpr (HALO) {
     h_img = tm / a.h_nb;
     h_oy0 = (tm - h_img * a.h_nb) * a.h_th;
@@ -536,6 +542,33 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
           T[row * BN + col] = v[i][j][r];
         }
     __syncthreads();
+    if constexpr (!HALO && BM * BN * 4 + 256 * 4 <= LDSB - 16) {
+      if (d.pool_rows) {
+        // fused avgpool + FC: column means of the tile's pool_rows valid rows,
+        // four row-interleaved partial sums per column, combined through LDS
+        constexpr int PARTS = 256 / BN;
+        float* red = T + BM * BN;
+        const int col = tid % BN, part = tid / BN;
+        float sum = 0.f;
+        for (int r = part; r < d.pool_rows; r += PARTS) sum += T[r * BN + (col ^ (((r >> 2) & 3) << 4))];
+        red[part * BN + col] = sum;
+        __syncthreads();
+        if (tid < BN) {
+          float tot = 0.f;
+#pragma unroll
+          for (int q = 0; q < PARTS; ++q) tot += red[q * BN + tid];
+          const int n = n0 + tid;
+          if (n < d.N) {
+            const float y = apply_act(tot / (float)d.pool_rows + (a.p.bias ? a.p.bias[n] : 0.f), d.act);
+            if (d.out_f32 || sizeof(typename TR::Out) == 4)
+              static_cast<float*>(a.p.C)[(size_t)tm * d.ldc + n] = y;
+            else
+              static_cast<_Float16*>(a.p.C)[(size_t)tm * d.ldc + n] = static_cast<_Float16>(y);
+          }
+        }
+        return;
+      }
+    }
     constexpr int G = BN / 8, RSTEP = 256 / G, ITEMS = BM / RSTEP;
     const int cg = tid % G, r0 = tid / G;
     const int nb = n0 + cg * 8;
@@ -1110,6 +1143,7 @@ void xcd_groups(const GemmDesc& d, Prec prec, int TM, int TN, int& gm, int& gn) 
 
 int plan_tiles(const GemmDesc& d, const Plan& pl) {
   if (pl.halo) return d.M / (d.OH * d.OW) * pl.nb * ((d.N + pl.bn - 1) / pl.bn);
+  if (d.pool_rows) return d.M / d.pool_rows * ((d.N + pl.bn - 1) / pl.bn);
   return ((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
 }
 
@@ -1127,6 +1161,7 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (k.forced) return finish_plan(k.plan, ksteps, ES);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
   const auto stages_for = [](int kt) { return kt >= 16 ? 3 : 2; };  // a deeper ring pays only on long K loops
+  if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES);  // one image per tile row
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
     const int T = k.target;
@@ -1246,6 +1281,8 @@ extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
 #endif
 
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
+  if (d.pool_rows && (d.conv || d.pool_rows > 64 || d.M % d.pool_rows))
+    throw std::invalid_argument("pooled GEMM: dense A, pool_rows <= 64 dividing M");
   switch (prec) {
     case Prec::F16:
       launch<(int)Prec::F16>(d, p, s);

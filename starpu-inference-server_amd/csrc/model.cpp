@@ -71,6 +71,8 @@ struct Workspace {
   size_t partial_floats = 0;
   int* counters = nullptr;  // split-K tickets (zeroed once; the reducer re-zeroes its slot)
   bool has_mask = false;
+  int final_buf = 6;  // ResNet: buffer holding the last stage's output
+  int final_hw = 0;   // ... and its pixels per image (avgpool window)
   std::map<int, hipGraphExec_t> graphs;
   ~Workspace() {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
@@ -663,6 +665,35 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   if (prof_) op_end(s);
 }
 
+// avgpool + fc as one GEMM over every pixel of the last stage with a
+// column-mean epilogue (GemmDesc::pool_rows): the split / fp16 / fp32 activation
+// is the A operand as is, so the pooled vector never goes through HBM.
+bool Model::pooled_fc(int hw) const { return hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
+
+void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s) {
+  GemmDesc d = linear_desc(fc_, B * hw, feat_, classes_);
+  d.pool_rows = hw;
+  d.out_f32 = true;
+  d.a_split = split_;
+  d.wplane = fc_.wplane;
+  const size_t es = f16_ ? 2 : 4;
+  if (prof_)
+    op_begin(s, "avgpool_fc_M" + std::to_string(B * hw) + "_N" + std::to_string(classes_) + "_K" +
+                    std::to_string(feat_),
+             2.0 * B * classes_ * (double)feat_,
+             (double)B * hw * feat_ * es + (double)fc_.n * fc_.k * es + (double)B * classes_ * 4);
+  GemmPtrs p;
+  p.A = act;
+  p.W = ptr<void>(fc_.w);
+  p.bias = ptr<float>(fc_.b);
+  p.C = out;
+  p.partial = ws.partial;
+  p.counters = ws.counters;
+  p.zeros = dblob_;
+  gemm(d, p, prec_, s);
+  if (prof_) op_end(s);
+}
+
 // ---------------------------------------------------------------------------
 // Workspaces
 // ---------------------------------------------------------------------------
@@ -828,12 +859,17 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       }
       H = H2;
     }
-    if (prof_) op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
-    if (split_)
-      avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
-    else
-      avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
-    if (prof_) op_end(s);
+    w.final_buf = cur;
+    w.final_hw = H * H;
+    if (!pooled_fc(H * H)) {  // else avgpool + fc run as one GEMM in the epilogue
+      if (prof_) op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
+      if (split_)
+        avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
+      else
+        avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+      if (prof_) op_end(s);
+      w.final_buf = 6;
+    }
   } else if (family_ == SPI_FAMILY_BERT) {
     const int S = S_in, T = B * S;
     float* hf = static_cast<float*>(w.bufs[0]);
@@ -898,7 +934,10 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
 
 void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
-    run_gemm(fc_, w.bufs[6], B, feat_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);
+    if (pooled_fc(w.final_hw))
+      run_pooled_fc(w.bufs[w.final_buf], B, w.final_hw, out[0], w, s);
+    else
+      run_gemm(fc_, w.bufs[6], B, feat_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const TfLayer& L = tf_.back();
     const int T = B * S;

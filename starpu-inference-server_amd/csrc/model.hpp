@@ -104,6 +104,8 @@ class Model {
                 hipStream_t s);
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
                 Act act, const void* res, Workspace& ws, hipStream_t s);
+  bool pooled_fc(int hw) const;
+  void run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s);
   size_t conv_partial(const ConvW& c, int B, int H, int W) const;
   size_t linear_partial(const LinearW& L, int M) const;
   template <typename P>

@@ -149,6 +149,34 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
   return check_launch();
 }
 
+int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, int32_t C, const void* W, int32_t N,
+                      const float* bias, float* y, int32_t act, void* workspace, void* stream) {
+  spi::Prec p;
+  if (!prec_of(precision, &p) || !x || !W || !y || !workspace || B <= 0 || HW <= 0 || HW > 64 || C <= 0 ||
+      N <= 0 || act < 0 || act > 2)
+    return fail("invalid avgpool_fc arguments");
+  if (precision == kSplitPrecision && C % 32) return fail("split avgpool_fc needs C a multiple of 32");
+  spi::GemmDesc d;
+  d.M = B * HW;
+  d.N = N;
+  d.K = C;
+  d.Kpad = spi::round_up_to(C, 64);
+  d.lda = C;
+  d.ldc = N;
+  d.ldr = N;
+  d.act = static_cast<spi::Act>(act);
+  d.out_f32 = true;
+  d.pool_rows = HW;
+  d.a_split = precision == kSplitPrecision;
+  spi::GemmPtrs ptrs = scratch(workspace);
+  ptrs.A = x;
+  ptrs.W = W;
+  ptrs.bias = bias;
+  ptrs.C = y;
+  spi::gemm(d, ptrs, p, static_cast<hipStream_t>(stream));
+  return check_launch();
+}
+
 int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias, void* ctx, int32_t B, int32_t S,
                      int32_t heads, float scale, void* stream) {
   if ((precision != 0 && precision != 1) || !qkv || !ctx || B <= 0 || S <= 0 || heads <= 0)

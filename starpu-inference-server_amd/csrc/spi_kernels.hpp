@@ -40,6 +40,12 @@ struct GemmDesc {
   // out_split: C is written split.
   bool a_split = false;
   bool out_split = false;
+  // Fused global average pool + linear layer (ResNet avgpool + fc): A holds
+  // pool_rows consecutive rows (pixels) per image; output row b of C is
+  // act(mean over image b's rows of A . W^T + bias).  Linearity lets the GEMM
+  // run over every pixel and average its own C tile (64 x 64 tiles, one image
+  // per tile row, pool_rows <= 64).  M = images x pool_rows.
+  int pool_rows = 0;
 };
 
 struct GemmPtrs {

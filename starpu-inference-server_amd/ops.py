@@ -121,3 +121,14 @@ def layernorm(prec, x, gamma, beta, eps, stream=None):
     _check(lib.spi_op_layernorm(PREC[prec], _ptr(x), _ptr(gamma), _ptr(beta), _ptr(yf), _ptr(yt), rows, D, eps,
                                 C.c_void_p(s)))
     return yf, yt
+
+
+def avgpool_fc(prec, x, W_packed, N_, bias=None, act=None, ws=None, stream=None):
+    """Fused global average pool + linear layer: x [B][HW][C] -> fp32 [B][N] (one launch)."""
+    B, HW, Cc = x.shape
+    out = torch.empty(B, N_, device=x.device, dtype=torch.float32)
+    ws = workspace(x.device) if ws is None else ws
+    s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+    _check(lib.spi_op_avgpool_fc(PREC[prec], _ptr(x), B, HW, Cc, _ptr(W_packed), N_, _ptr(bias), _ptr(out), ACT[act],
+                                 _ptr(ws), C.c_void_p(s)))
+    return out

@@ -178,3 +178,23 @@ def test_split_layout_rejects_bad_shapes(ops):
     wp = ops.pack_weight("fp16x3s", np.zeros((32, 9 * 16), np.float32))
     with pytest.raises(ops.OpError):
         ops.conv2d("fp16x3s", x, wp, 32, 3, 3, 1, 1)  # Cin 16 < 32
+
+
+@pytest.mark.parametrize("prec", PRECS + ["fp16x3s"])
+@pytest.mark.parametrize("B,HW,C,N", [(8, 49, 512, 1000), (3, 4, 512, 1000), (2, 49, 2048, 1000), (5, 64, 96, 70)])
+def test_avgpool_fc_fused(ops, prec, B, HW, C, N):
+    """ResNet's avgpool + fc as one GEMM launch (GemmDesc::pool_rows): the column mean of each
+    image's pixel rows of A . W^T, plus bias -- vs fp32 torch mean-then-linear."""
+    if prec == "fp16x3s" and C % 32:
+        pytest.skip("split layout needs C % 32 == 0")
+    g = torch.Generator().manual_seed(B * HW + C)
+    x = torch.rand(B, HW, C, generator=g)
+    W = torch.randn(N, C, generator=g) / C ** 0.5
+    b = torch.randn(N, generator=g)
+    base = "fp16x3" if prec == "fp16x3s" else prec
+    xin = ops.to_split(x) if prec == "fp16x3s" else x.to(ops.act_dtype(prec))
+    ref = xin.float().mean(1) if prec in ("fp32", "fp16") else x.mean(1)
+    ref = ref @ (W.half().float() if prec == "fp16" else W).T + b
+    out = ops.avgpool_fc(prec, xin.cuda(), ops.pack_weight(base, W), N, bias=b.cuda())
+    err = normalized_max_error(out.cpu().numpy(), ref.numpy())
+    assert err < TOL[base], f"{prec} B{B} HW{HW} C{C} N{N}: {err:.3e}"
