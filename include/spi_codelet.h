@@ -59,7 +59,7 @@ extern "C" {
  * reads only id, ptr, nx and elemsize, exactly like the reference
  * (starpu_setup.cpp:515-542, tensor_builder.cpp:120).  The id values follow
  * StarPU 1.4's enum starpu_data_interface_id; a build against the real
- * <starpu.h> static_asserts them (see spi_starpu_adapter.cpp).
+ * <starpu.h> static_asserts them (csrc/spi_starpu_adapter.cpp, -DSPI_WITH_STARPU).
  * ------------------------------------------------------------------------- */
 enum spi_interface_id {
   SPI_STARPU_MATRIX_INTERFACE_ID = 0,

@@ -331,23 +331,7 @@ void spi_cpu_inference_func(void** buffers, void* cl_arg) {
   a->codelet_end_ns = now_ns();
 }
 
-int spi_codelet_init(void* starpu_codelet) {
-#ifdef SPI_WITH_STARPU
-  auto* cl = static_cast<struct starpu_codelet*>(starpu_codelet);
-  if (!cl) return SPI_ERR_INVALID_ARGUMENT;
-  starpu_codelet_init(cl);
-  cl->nbuffers = STARPU_VARIABLE_NBUFFERS;
-  cl->type = STARPU_FORKJOIN;
-  cl->max_parallelism = INT_MAX;
-  cl->cpu_funcs[0] = &spi_cpu_inference_func;
-  cl->hip_funcs[0] = &spi_hip_inference_func;
-  cl->hip_flags[0] = STARPU_HIP_ASYNC;
-  return SPI_OK;
-#else
-  (void)starpu_codelet;
-  return SPI_ERR_UNSUPPORTED;
-#endif
-}
+// spi_codelet_init: spi_starpu_adapter.cpp (the StarPU descriptor + layout static_asserts).
 
 // ---------------------------------------------------------------------------
 // Model replicas

@@ -371,3 +371,16 @@ def test_runtime_rejects_invalid_config_without_touching_a_device(spi):
     assert not spi.lib.spi_runtime_create(C.byref(cfg), err, 128)  # no replica for the device
     assert b"missing replica" in err.value
     assert spi.lib.spi_runtime_submit(None, 0, 1, None, None, rt.DONE_FN(), None) == spi._native.SPI_ERR_INVALID_ARGUMENT
+
+
+def test_starpu_adapter_compiles_without_starpu(tmp_path):
+    """csrc/spi_starpu_adapter.cpp builds in the default (no StarPU) configuration, and asking
+    for the StarPU build without <starpu.h> fails at compile time with a clear message instead of
+    guessing the interface layout."""
+    import subprocess
+    src = os.path.join(ROOT, "starpu-inference-server_amd", "csrc", "spi_starpu_adapter.cpp")
+    ok = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", src], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
+    bad = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-DSPI_WITH_STARPU", src], capture_output=True,
+                         text=True)
+    assert bad.returncode != 0 and "SPI_WITH_STARPU needs <starpu.h>" in bad.stderr

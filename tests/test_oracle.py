@@ -96,3 +96,43 @@ def test_oracle_reproduces_model_fixtures(zoo, name):
     assert normalized_max_error(out, ref) < 1e-5
     if ref.ndim == 2:
         assert top1_agreement(out, ref) == 1.0
+
+
+# Graph fidelity of the oracle's ResNet / ViT restatements (torchvision itself is
+# not importable here).  torchvision publishes, in each pretrained weights enum's
+# metadata, the parameter count and the multiply-add count ("_ops", GMACs at 224^2)
+# of exactly the graphs models/import_resnet.py and models/import_vit.py export:
+#   ResNet18_Weights.IMAGENET1K_V1   num_params 11,689,512   _ops 1.814
+#   ResNet152_Weights.IMAGENET1K_V1  num_params 60,192,808   _ops 11.514
+#   ViT_L_16_Weights.IMAGENET1K_V1   num_params 304,326,632  _ops 61.555
+# Matching both (per-tensor names follow torchvision's state_dict keys) pins the
+# layer structure the parity tests compare against; the arithmetic per layer is
+# ATen's.  BERT uses transformers' own BertModel, so it needs no such pin.
+TORCHVISION_META = {"resnet18": (11_689_512, 1.814), "resnet152": (60_192_808, 11.514),
+                    "vit_l_16": (304_326_632, 61.555)}
+
+
+@pytest.mark.parametrize("name", sorted(TORCHVISION_META))
+def test_restated_graphs_match_torchvision_metadata(zoo, name):
+    from torch.utils.flop_counter import FlopCounterMode
+
+    params, gmacs = TORCHVISION_META[name]
+    model = zoo.build(name, seed=0)
+    assert sum(p.numel() for p in model.parameters()) == params
+    sd = model.state_dict()
+    if name.startswith("resnet"):
+        for key in ("conv1.weight", "bn1.running_var", "layer1.0.conv1.weight", "layer4.0.downsample.0.weight",
+                    "layer4.0.downsample.1.running_mean", "fc.weight", "fc.bias"):
+            assert key in sd, key
+    else:
+        for key in ("class_token", "conv_proj.weight", "encoder.pos_embedding",
+                    "encoder.layers.encoder_layer_23.self_attention.in_proj_weight",
+                    "encoder.layers.encoder_layer_23.mlp.3.weight", "encoder.ln.weight", "heads.head.weight"):
+            assert key in sd, key
+    # grad mode on: nn.MultiheadAttention's fused inference fast path is invisible to the counter
+    with FlopCounterMode(display=False) as fc:
+        model(torch.zeros(1, 3, 224, 224))
+    # torchvision's _ops counts the conv / linear / attention-matmul multiply-adds; the counter
+    # does not see scaled_dot_product_attention's CPU matmuls, added here (QK^T and PV per layer)
+    attn = 24 * 2 * 197 * 197 * 1024 / 1e9 if name == "vit_l_16" else 0.0
+    assert abs(fc.get_total_flops() / 2e9 + attn - gmacs) / gmacs < 2e-3
