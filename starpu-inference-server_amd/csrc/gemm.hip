@@ -113,11 +113,17 @@ struct KArgs {
   int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
   int vec_ok;       // C / residual rows allow 16-byte vectors of 8 elements (epilogue)
   int xg_m, xg_n;   // XCD rectangles: tile rows in xg_m groups x tile columns in xg_n groups
-  // halo conv (kConvHalo): tiles are bands of h_th output rows x the full width of
-  // one image; h_nb bands per image; the band's input rows (+1 pixel of padding
-  // around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel blocks,
-  // h_bps of them per split-K slice
-  int h_th, h_nb, h_hwp, h_hp, h_nblk, h_bps;
+  // halo conv (kConvHalo): tile row block tm is the band of h_th "virtual" output
+  // rows u in [tm * h_th, (tm + 1) * h_th) x the full width.  Virtual rows stack the
+  // images with a period of h_period rows: image u / h_period, output row
+  // u % h_period - h_off (valid when in [0, OH)).  Aligned bands (h_off 0,
+  // h_period = bands per image x h_th) stay inside one image; stacked bands
+  // (h_off 1, h_period = OH + 2: a zero row above and below every image) may span
+  // several images, so one tile can cover whole small maps of several images and
+  // the weights are re-read by fewer tiles.  The band's input rows (+1 pixel of
+  // padding around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel
+  // blocks, h_bps of them per split-K slice
+  int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
 };
 
 template <int MODE>
@@ -205,17 +211,17 @@ __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
   return *reinterpret_cast<const u32x4*>(img + row * RB + ((c ^ (row & (CPR - 1))) << 4));
 }
 
-// Split-K is compiled into the 64x64 tiles only (no plan rule splits a larger
-// tile; its reducer alone cost 36-120 VGPRs there).  Launch bounds ask for the
-// occupancy each tile reaches within its registers: 4 / 3 / 2 waves per SIMD.
-template <int BM, int BN>
-constexpr bool kSplitK = BM == 64 && BN == 64;
-
 // A-operand kinds: dense rows; conv with one (kh, kw) tap per k-step (Cin >= the
 // k-step: scalar tap walk + per-row tap mask); conv in general (per-chunk taps:
 // the stem); 3x3/s1/p1 conv from an LDS-resident input band (kConvHalo, below).
 // Separate instantiations keep each kind's loop free of the others.
 enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS = 4 };
+
+// Split-K is compiled into the 64x64 tiles and the halo kinds (no plan rule splits
+// another large tile; the reducer costs 36-120 VGPRs there).  Launch bounds ask
+// for the occupancy each tile reaches within its registers: 4 / 3 / 2 waves per SIMD.
+template <int BM, int BN, int KIND>
+constexpr bool kSplitK = (BM == 64 && BN == 64) || KIND == kConvHalo || KIND == kConvHaloS;
 
 // kConvHalo.  An implicit-GEMM conv stages each (tap, channel block) A tile
 // separately: every input pixel crosses the CU nine times, and the vector-memory
@@ -229,36 +235,44 @@ enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS =
 // buffer: HQ DMA instructions per wave x 4 waves x 8 pixels.
 // kConvHaloS: the 64-row kind with 96-pixel buffers (14- and 7-wide layers):
 // 48 KiB of LDS instead of 56, three workgroups per CU instead of two.
-template <int BM, int KIND>
-constexpr int kHaloHQ = KIND == kConvHaloS ? 3 : BM == 64 ? 4 : 8;
+// NW = 8 (the 256-row kind, 4 x 2 waves): 6 pieces per wave = 384-pixel buffers.
+template <int BM, int KIND, int NW>
+constexpr int kHaloHQ = KIND == kConvHaloS ? 3 : NW == 8 ? 6 : BM == 64 ? 4 : 8;
 template <int KIND>
 constexpr bool kIsHalo = KIND == kConvHalo || KIND == kConvHaloS;
-template <int BM, int BN, int STAGES, int KIND>
-constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND> * 32 * 128 + 16
+template <int BM, int BN, int STAGES, int KIND, int NW>
+constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND, NW> * NW * 8 * 128 + 16
                                         : STAGES * (BM + BN) * 128 + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
-// size, capped by what the tile's LDS ring allows (one wave per SIMD per block,
-// 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
-template <int BM, int BN, int STAGES, int KIND>
-constexpr int kMinWaves = std::max(1, std::min(BM * BN <= 64 * 64 ? 4 : BM * BN <= 128 * 64 ? 3 : 2,
-                                               (160 * 1024) / kLdsBytes<BM, BN, STAGES, KIND>));
+// size per wave, capped by what the tile's LDS ring allows (NW / 4 waves per SIMD
+// per block, 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
+template <int BM, int BN, int STAGES, int KIND, int NW>
+constexpr int kMinWaves = std::max(
+    1, std::min(BM * BN * 4 / NW <= 64 * 64 ? 4 : BM * BN * 4 / NW <= 128 * 64 ? 3 : 2,
+                (160 * 1024) / kLdsBytes<BM, BN, STAGES, KIND, NW> * NW / 4));
 
-template <int MODE, int BM, int BN, int STAGES, int KIND>
-__global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_kernel(KArgs a) {
+// NW waves per workgroup in an (NW / 2) x 2 grid over the tile: wave (wm, wn)
+// owns rows [wm * BM / (NW / 2), ...) x columns [wn * BN / 2, ...).
+template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel(KArgs a) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
+  constexpr int NT = 64 * NW;  // threads per workgroup
+  static_assert(NW == 4 || (NW == 8 && HALO), "8-wave workgroups: halo kinds only");
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
   constexpr int CPR = RB / 16;             // chunks per image row
   constexpr int RPI = 64 / CPR;            // image rows per 1-KiB DMA instruction
   constexpr int IMG = (HALO ? BN : BM + BN) * RB;  // bytes per ring stage (halo: W only)
-  constexpr int AQ = BM / RPI / 4, BQ = BN / RPI / 4;  // DMA instructions per wave per step
+  constexpr int AQ = BM / RPI / NW, BQ = BN / RPI / NW;  // DMA instructions per wave per step
+  static_assert(HALO || AQ * RPI * NW == BM, "A image rows per wave");
+  static_assert(BQ * RPI * NW == BN, "W image rows per wave");
   constexpr int QPS = (HALO ? 0 : AQ) + BQ;
-  constexpr int HQ = HALO ? kHaloHQ<BM, KIND> : 1;          // halo DMA instructions per wave per block
-  constexpr int HBUF = HALO ? HQ * 4 * RPI * RB : 0;  // bytes per halo buffer
-  constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND>;
+  constexpr int HQ = HALO ? kHaloHQ<BM, KIND, NW> : 1;  // halo DMA instructions per wave per block
+  constexpr int HBUF = HALO ? HQ * NW * RPI * RB : 0;  // bytes per halo buffer
+  constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND, NW>;
   static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
   static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -294,20 +308,33 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
     tn = nlo + loc / mi;
   }
   const int n0 = tn * BN;
-  // m_lim: first row past this tile's valid rows (halo bands end at the image)
-  int m0 = tm * BM, m_lim = d.M, h_img = 0, h_oy0 = 0;
+  // m_lim: first row past this tile's valid rows.  Halo tiles map their rows to
+  // output rows through the virtual-row bands (halo_m below) instead.
+  int m0 = tm * BM, m_lim = d.M;
   if constexpr (!HALO) {
     if (d.pool_rows) {  // fused avgpool + FC: tile row tm = image tm's pixels
       m0 = tm * d.pool_rows;
       m_lim = m0 + d.pool_rows;
     }
   }
+  // halo: first virtual output row of the band; halo_m(r) = output row of tile row
+  // r (-1: a padding row of the virtual layout, or past the last image)
+  const int h_u0 = HALO ? tm * a.h_th : 0;
   if constexpr (HALO) {
-    h_img = tm / a.h_nb;
-    h_oy0 = (tm - h_img * a.h_nb) * a.h_th;
-    m0 = (h_img * d.OH + h_oy0) * d.OW;
-    m_lim = m0 + min(a.h_th, d.OH - h_oy0) * d.OW;
+    if (!a.h_off) {  // aligned band: contiguous output rows [m0, m_lim) of one image
+      const int img = h_u0 / a.h_period, oy0 = h_u0 - img * a.h_period;
+      m0 = (img * d.OH + oy0) * d.OW;
+      m_lim = m0 + min(a.h_th, d.OH - oy0) * d.OW;
+    }
   }
+  [[maybe_unused]] auto halo_m = [&](int r) {
+    const int ty = r / d.OW, tx = r - ty * d.OW;
+    const int u = h_u0 + ty;
+    const int img = u / a.h_period;
+    const int oy = u - img * a.h_period - a.h_off;
+    return (ty < a.h_th && img < d.M / (d.OH * d.OW) && (unsigned)oy < (unsigned)d.OH) ? (img * d.OH + oy) * d.OW + tx
+                                                                                      : -1;
+  };
   const int kbeg = blockIdx.y * a.k_per_split;
   const int kend = min(d.Kpad, kbeg + a.k_per_split);
   // halo: channel blocks [h_b0, h_b1) of this split-K slice, 9 taps each
@@ -379,25 +406,40 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   // padding or past the halo.  Fragment side: h_row[i] = halo pixel of tap (0, 0)
   // for this lane's row of A fragment i (rows past the band read pixel 0; their
   // results are never stored).
+  // Virtual input rows: aligned bands read rows of their own image only (row
+  // oy0 - 1 + hy); stacked bands read virtual row u0 - 1 + hy, i.e. image
+  // (u0 - 1 + hy) / period, row (u0 - 1 + hy) % period - 1 (the padding rows of the
+  // stacked layout and rows past the last image read zeros).
+  constexpr int WTM_ = BM / (NW / 2);  // rows per wave
   [[maybe_unused]] const AT* h_src[HQ];
   [[maybe_unused]] bool h_ok[HQ];
-  [[maybe_unused]] int h_row[BM / 32];
+  [[maybe_unused]] int h_row[WTM_ / 16];
   if constexpr (HALO) {
+    const int imgs = d.M / (d.OH * d.OW);
 #pragma unroll
     for (int q = 0; q < HQ; ++q) {
       const int p = (wave * HQ + q) * RPI + lane / CPR;
       const int c = slot ^ (p & (CPR - 1));
       const int hy = p / a.h_hwp, hx = p - hy * a.h_hwp;
-      const int iy = h_oy0 * d.stride - d.pad + hy, ix = hx - d.pad;
-      h_ok[q] = p < a.h_hp && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      h_src[q] = Ap + ((size_t)(h_img * d.H + (h_ok[q] ? iy : 0)) * d.W + (h_ok[q] ? ix : 0)) * d.Cin + c * EPC;
+      int img, iy;
+      if (a.h_off) {
+        const int vy = h_u0 - 1 + hy;
+        img = vy < 0 ? imgs : vy / a.h_period;
+        iy = vy - img * a.h_period - 1;
+      } else {
+        img = h_u0 / a.h_period;
+        iy = h_u0 - img * a.h_period - 1 + hy;
+      }
+      const int ix = hx - 1;
+      h_ok[q] = p < a.h_hp && img < imgs && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      h_src[q] = Ap + ((size_t)((h_ok[q] ? img : 0) * d.H + (h_ok[q] ? iy : 0)) * d.W + (h_ok[q] ? ix : 0)) * d.Cin +
+                 c * EPC;
     }
-    const int rows = m_lim - m0;
 #pragma unroll
-    for (int i = 0; i < BM / 32; ++i) {
-      const int r = (wave >> 1) * (BM / 2) + i * 16 + (lane & 15);
+    for (int i = 0; i < WTM_ / 16; ++i) {
+      const int r = (wave >> 1) * WTM_ + i * 16 + (lane & 15);
       const int ty = r / d.OW, tx = r - ty * d.OW;
-      h_row[i] = r < rows ? ty * d.stride * a.h_hwp + tx * d.stride : 0;
+      h_row[i] = ty < a.h_th ? ty * a.h_hwp + tx : 0;
     }
   }
   auto issue_halo = [&](int blk, int buf) {
@@ -503,7 +545,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 
   const int fr = lane & 15, fq = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int WTM = BM / (NW / 2), WTN = BN / 2;
   constexpr int TI = WTM / 16, TJ = WTN / 16;
   floatx4 acc[TI][TJ];
 #pragma unroll
@@ -546,7 +588,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
       if (d.pool_rows) {
         // fused avgpool + FC: column means of the tile's pool_rows valid rows,
         // four row-interleaved partial sums per column, combined through LDS
-        constexpr int PARTS = 256 / BN;
+        constexpr int PARTS = NT / BN;
         float* red = T + BM * BN;
         const int col = tid % BN, part = tid / BN;
         float sum = 0.f;
@@ -569,10 +611,18 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
         return;
       }
     }
-    constexpr int G = BN / 8, RSTEP = 256 / G, ITEMS = BM / RSTEP;
+    constexpr int G = BN / 8, RSTEP = NT / G, ITEMS = BM / RSTEP;
     const int cg = tid % G, r0 = tid / G;
     const int nb = n0 + cg * 8;
     const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
+    // output row of tile row `row`, -1 when it is not stored
+    auto row_m = [&](int row) -> int {
+      if constexpr (HALO) {
+        if (a.h_off) return halo_m(row);
+      }
+      const int m = m0 + row;
+      return m < m_lim ? m : -1;
+    };
     auto tile_vals = [&](int row, float (&y)[8]) {
       const float* src = T + row * BN + ((cg * 8) ^ (((row >> 2) & 3) << 4));
       const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
@@ -617,7 +667,8 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
         if (a.p.res) {
 #pragma unroll
           for (int it = 0; it < CH; ++it) {
-            const int m = min(m0 + r0 + (c0 + it) * RSTEP, m_lim - 1);
+            const int mr = row_m(r0 + (c0 + it) * RSTEP);
+            const int m = mr < 0 ? 0 : mr;  // skipped rows load row 0 (always valid)
             if constexpr (MODE == kF16X3S) {
               const _Float16* R = static_cast<const _Float16*>(a.p.res) + split_idx(m, nb, d.ldr);
               const half8 hi = *reinterpret_cast<const half8*>(R);
@@ -651,8 +702,8 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
         finish_act(y);
 #pragma unroll
         for (int it = 0; it < CH; ++it) {
-          const int m = m0 + r0 + (c0 + it) * RSTEP;
-          if (m >= m_lim) continue;
+          const int m = row_m(r0 + (c0 + it) * RSTEP);
+          if (m < 0) continue;
           if (fmt == 2) {
             half8 hi, lo;
 #pragma unroll
@@ -681,8 +732,8 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 #pragma unroll
     for (int e = 0; e < 8; ++e) b[e] = (a.p.bias && nb + e < d.N) ? a.p.bias[nb + e] : 0.f;
     for (int it = 0; it < ITEMS; ++it) {
-      const int row = r0 + it * RSTEP, m = m0 + row;
-      if (m >= m_lim) continue;
+      const int row = r0 + it * RSTEP, m = row_m(row);
+      if (m < 0) continue;
       float y[8];
       tile_vals(row, y);
       for (int e = 0; e < 8; ++e) {
@@ -952,15 +1003,15 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
     g[4] = (unsigned long long)nsteps;
   }
 #endif
-  if (!kSplitK<BM, BN> || gridDim.y == 1) {
+  if (!kSplitK<BM, BN, KIND> || gridDim.y == 1) {
     finish(acc);
     return;
   }
-  if constexpr (kSplitK<BM, BN>) {
+  if constexpr (kSplitK<BM, BN, KIND>) {
 
   // ---- split-K: publish this slice's slab, the last arriver reduces -------
   // Slabs are written in fragment order (thread tid's accumulator (i, j) is 16
-  // contiguous bytes at ((i*TJ + j)*256 + tid)*16), write-through (sc1) so no
+  // contiguous bytes at ((i*TJ + j)*NT + tid)*16), write-through (sc1) so no
   // release fence is needed; the ticket is a relaxed agent-scope atomic; the
   // reducer reads every slab with sc1 loads.  Same thread <-> (m, n) map as above.
   const int splits = gridDim.y;
@@ -972,7 +1023,7 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const int off = (blockIdx.y * SLAB + ((i * TJ + j) * 256 + tid) * 4) * 4;
+      const int off = (blockIdx.y * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
     }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -984,26 +1035,29 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
   }
   __syncthreads();
   if (!*s_flag) return;
-  // Two splits' slabs in flight per round; loads past the last slab fall
-  // outside the descriptor's range and return 0 (no branch, no per-load wait).
+  // ZR splits' slabs in flight per round (two for the small tiles, one when a
+  // slab is 8+ fragments per thread); loads past the last slab fall outside the
+  // descriptor's range and return 0 (no branch, no per-load wait).  Slabs are
+  // summed in split order whichever slice arrives last: deterministic results.
+  constexpr int ZR = TI * TJ <= 4 ? 2 : 1;
   floatx4 sum[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int z0 = 0; z0 < splits; z0 += 2) {
-    floatx4 v[2][TI][TJ];
+  for (int z0 = 0; z0 < splits; z0 += ZR) {
+    floatx4 v[ZR][TI][TJ];
 #pragma unroll
-    for (int zz = 0; zz < 2; ++zz)
+    for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * 256 + tid) * 4) * 4;
+          const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
           v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
         }
 #pragma unroll
-    for (int zz = 0; zz < 2; ++zz)
+    for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -1015,8 +1069,10 @@ __global__ __launch_bounds__(256, (kMinWaves<BM, BN, STAGES, KIND>)) void gemm_k
 
 struct Plan {
   int bm, bn, stages, splits, k_per_split;
-  // kConvHalo: output rows per band, bands per image, channel blocks per slice
-  int halo = 0, th = 0, nb = 0, bps = 0;
+  // kConvHalo: waves per workgroup, virtual output rows per band, the virtual-row
+  // period (rows per image) and offset (KArgs::h_off), band count, channel blocks
+  // per slice
+  int halo = 0, nw = 4, th = 0, period = 0, off = 0, tiles_m = 0, bps = 0;
 };
 
 int estep_of(Prec prec) {
@@ -1038,6 +1094,15 @@ struct Knobs {
   int max_split = 0, stages = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
   int halo_stages = 3, halo_minh = 14;
+  int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
+  int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
+  bool halo_stacked = false;
+  struct HaloPick {
+    int ow, bm;
+    bool stacked;
+  };
+  HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
+  int n_halo_map = 0;
   int xcd2d = 1;  // 2-D tile -> XCD rectangles (xcd_groups)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
 
@@ -1062,6 +1127,28 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_XCD2D"); e && *e) k.xcd2d = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
+    // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
+    // (OW 0 = any other width; rows 0 = not a halo conv)
+    if (std::strchr(e, ':')) {
+      for (const char* q = e; q && *q;) {
+        int ow = 0, bm = 0;
+        char mode = 'a';
+        if (std::sscanf(q, "%d:%d,%c", &ow, &bm, &mode) >= 2 && k.n_halo_map < 8)
+          k.halo_map[k.n_halo_map++] = {ow, bm, mode == 's'};
+        q = std::strchr(q, ';');
+        if (q) ++q;
+      }
+    } else {
+      int bm = 0;
+      char mode = 'a';
+      if (std::sscanf(e, "%d,%c", &bm, &mode) >= 1 && (bm == 64 || bm == 128 || bm == 256)) {
+        k.halo_bm = bm;
+        k.halo_stacked = mode == 's';
+      }
+    }
+  }
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SPI_GEMM_STAGES"); e && *e) k.stages = std::max(2, std::min(4, std::atoi(e)));
   return k;
@@ -1085,36 +1172,75 @@ Plan finish_plan(Plan pl, int ksteps, int ES) {
 }
 
 // kConvHalo plan for 3x3/s1/p1 convs with whole channel blocks (split activations
-// in F16X3): 128-row tiles when the output is wider than 32 pixels (the 56-wide
-// layers: two rows per band), else 64; as many whole output rows per band as fit
-// the tile and the halo buffer; split-K over channel blocks (64-row tiles only)
-// up to ~T workgroups.  halo = 0 when the conv is not eligible.
+// in F16X3).  Candidates (all 64 columns wide):
+//   64 rows, 4 waves (kConvHaloS when the halo fits 96 pixels, else 128-pixel buffers)
+//   128 rows, 4 waves (256-pixel buffers); 256 rows, 8 waves (384-pixel buffers)
+// each with aligned bands (whole output rows of one image) or stacked bands
+// (virtual rows spanning images, for maps too small to fill a tile).  th = as many
+// (virtual) rows per band as fit the tile and the halo buffer; split-K over
+// channel blocks up to ~T workgroups.  The default picks aligned 128 rows for maps
+// wider than 32 pixels, else aligned 64 (the round-1 rule) -- SPI_GEMM_HALO_CFG =
+// "rows,a|s" forces a candidate (tools/gemm_bench.py sweeps).  halo = 0 when the
+// conv is not eligible.
+Plan halo_candidate(const GemmDesc& d, Prec prec, int T, int bm, bool stacked, int smax) {
+  Plan no{};
+  const int ES = estep_of(prec);
+  const int nw = bm == 256 ? 8 : 4;
+  const int cap = (bm == 256 ? 6 * 8 : bm == 128 ? 8 * 4 : 4 * 4) * 8;  // kHaloHQ x NW x 8 pixels
+  const int imgs = d.M / (d.OH * d.OW);
+  int th = stacked ? bm / d.OW : std::min(bm / d.OW, d.OH);
+  while (th > 0 && (th + 2) * (d.W + 2) > cap) --th;
+  if (th == 0) return no;
+  const bool small = bm == 64 && (th + 2) * (d.W + 2) <= 3 * 32;  // kConvHaloS
+  const int nblk = d.Cin / ES;
+  Plan h{bm, 64, knobs().halo_stages, 1, 0};
+  h.nw = nw;
+  h.th = th;
+  if (stacked) {
+    h.off = 1;
+    h.period = d.OH + 2;
+    h.tiles_m = (imgs * h.period + th - 1) / th;
+  } else {
+    const int nb = (d.OH + th - 1) / th;
+    h.off = 0;
+    h.period = nb * th;
+    h.tiles_m = imgs * nb;
+  }
+  const int tiles = h.tiles_m * (d.N / 64);
+  int sp = 1;
+  if (tiles < T) sp = std::min({(T + tiles - 1) / tiles, nblk, smax});
+  if (knobs().max_split) sp = std::min(sp, knobs().max_split);
+  const int bps = (nblk + sp - 1) / sp;
+  h.splits = (nblk + bps - 1) / bps;
+  h.halo = small ? 2 : 1;
+  h.bps = bps;
+  return h;
+}
+
 Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
   Plan no{};
   const int ES = estep_of(prec);
   if (!knobs().halo || knobs().forced || !d.conv || d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 ||
-      d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W ||
-      d.OH < knobs().halo_minh)
+      d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W)
     return no;
+  if (knobs().halo_bm) return halo_candidate(d, prec, T, knobs().halo_bm, knobs().halo_stacked, 1 << 20);
+  for (int i = 0; i < knobs().n_halo_map; ++i) {
+    const auto& hm = knobs().halo_map[i];
+    if (hm.ow == d.OW || hm.ow == 0) {
+      if (hm.bm != 64 && hm.bm != 128 && hm.bm != 256) return no;
+      return halo_candidate(d, prec, T, hm.bm, hm.stacked, 1 << 20);
+    }
+  }
+  if (d.OH < knobs().halo_minh) return no;
+  // Under the serving load (four worker streams) the implicit GEMM's many small,
+  // LDS-light workgroups keep more kernels co-resident than the halo kinds'
+  // 56-90 KiB ones: ResNet-18 bs8 59.3k vs 57.0k inf/s, ResNet-152 bs32 10.7k vs
+  // 10.0k (tools/policy_sweep.py).  The halo kinds pay where the grid
+  // is small and one forward's latency dominates (ResNet-18 bs1: 13.2k vs 12.1k).
+  const auto ceil_div = [](int x, int y) { return (x + y - 1) / y; };
+  if (ceil_div(d.M, 64) * ceil_div(d.N, 64) >= knobs().halo_maxtiles) return no;
   const int bm = d.OW > 32 ? 128 : 64;
-  const int cap = (bm == 64 ? 4 : 8) * 32;  // halo pixels per buffer (kHaloHQ x 4 waves x 8)
-  int th = std::min(bm / d.OW, d.OH);
-  while (th > 0 && (th + 2) * (d.W + 2) > cap) --th;
-  if (th == 0) return no;
-  const bool small = bm == 64 && (th + 2) * (d.W + 2) <= 3 * 32;  // kConvHaloS
-  const int imgs = d.M / (d.OH * d.OW);
-  const int nb = (d.OH + th - 1) / th, nblk = d.Cin / ES;
-  const int tiles = imgs * nb * (d.N / 64);
-  int sp = 1;
-  if (bm == 64 && tiles < T) sp = std::min((T + tiles - 1) / tiles, nblk);
-  const int bps = (nblk + sp - 1) / sp;
-  sp = (nblk + bps - 1) / bps;
-  Plan h{bm, 64, knobs().halo_stages, sp, 0};
-  h.halo = small ? 2 : 1;
-  h.th = th;
-  h.nb = nb;
-  h.bps = bps;
-  return h;
+  return halo_candidate(d, prec, T, bm, false, bm == 64 ? 1 << 20 : 1);  // round 1: only 64-row tiles split
 }
 
 // XCD rectangles (gemm_kernel's tile decode): the row x column group split
@@ -1142,7 +1268,7 @@ void xcd_groups(const GemmDesc& d, Prec prec, int TM, int TN, int& gm, int& gn) 
 }
 
 int plan_tiles(const GemmDesc& d, const Plan& pl) {
-  if (pl.halo) return d.M / (d.OH * d.OW) * pl.nb * ((d.N + pl.bn - 1) / pl.bn);
+  if (pl.halo) return pl.tiles_m * ((d.N + pl.bn - 1) / pl.bn);
   if (d.pool_rows) return d.M / d.pool_rows * ((d.N + pl.bn - 1) / pl.bn);
   return ((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
 }
@@ -1222,12 +1348,17 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   if (pl.halo) {
     if constexpr (MODE != (int)Prec::F16X3) {  // fp32 A is split at fragment read: not a halo mode
       a.h_th = pl.th;
-      a.h_nb = pl.nb;
+      a.h_period = pl.period;
+      a.h_off = pl.off;
       a.h_hwp = d.W + 2 * d.pad;
       a.h_hp = (pl.th + 2) * a.h_hwp;
       a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
       a.h_bps = pl.bps;
-      if (pl.bm == 128 && pl.stages == 4)
+      if (pl.bm == 256 && pl.stages == 4)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 4, kConvHalo, 8>), grid, dim3(512), 0, s, a);
+      else if (pl.bm == 256)
+        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, a);
+      else if (pl.bm == 128 && pl.stages == 4)
         hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 4, kConvHalo>), grid, dim3(256), 0, s, a);
       else if (pl.bm == 128)
         hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);

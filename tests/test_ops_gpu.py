@@ -198,3 +198,57 @@ def test_avgpool_fc_fused(ops, prec, B, HW, C, N):
     out = ops.avgpool_fc(prec, xin.cuda(), ops.pack_weight(base, W), N, bias=b.cuda())
     err = normalized_max_error(out.cpu().numpy(), ref.numpy())
     assert err < TOL[base], f"{prec} B{B} HW{HW} C{C} N{N}: {err:.3e}"
+
+
+# ---- halo-band candidates (SPI_GEMM_HALO_CFG): aligned / stacked bands, 64 / 128 / 256-row tiles ----
+
+@pytest.fixture
+def halo_cfg(ops):
+    import os
+
+    def set_cfg(cfg):
+        if cfg:
+            os.environ["SPI_GEMM_HALO_CFG"] = cfg
+        else:
+            os.environ.pop("SPI_GEMM_HALO_CFG", None)
+        ops.lib.spi_debug_gemm_reload_env()
+
+    yield set_cfg
+    set_cfg("")
+
+
+@pytest.mark.parametrize("cfg", ["64,a", "64,s", "128,a", "128,s", "256,a", "256,s"])
+@pytest.mark.parametrize("B,H,cin,cout", [(8, 7, 512, 512), (3, 7, 64, 64), (2, 14, 128, 128), (3, 28, 64, 128),
+                                          (1, 56, 64, 64), (5, 9, 32, 64), (4, 13, 64, 64)])
+def test_conv_halo_candidates_split_layout(ops, halo_cfg, cfg, B, H, cin, cout):
+    """Every halo candidate (bands spanning images in the stacked mode, split-K over
+    channel blocks, the 8-wave 256-row kind) against an fp32 conv on the split values."""
+    g = torch.Generator().manual_seed(B * 131 + H + cin + cout)
+    x = torch.randn(B, H, H, cin, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g)
+    r = torch.randn(B, H, H, cout, generator=g)
+    xs = ops.to_split(x)
+    ref = F.conv2d(ops.from_split(xs).permute(0, 3, 1, 2), w, b, 1, 1).permute(0, 2, 3, 1)
+    ref = F.relu(ref + ops.from_split(ops.to_split(r)))
+    wp = ops.pack_weight("fp16x3s", ops.conv_weight_matrix(w, cin))
+    halo_cfg(cfg)
+    out = ops.conv2d("fp16x3s", xs.cuda(), wp, cout, 3, 3, 1, 1, bias=b.cuda(), act="relu",
+                     residual=ops.to_split(r).cuda())
+    err = normalized_max_error(ops.from_split(out.cpu()).numpy(), ref.numpy())
+    assert err < 1e-5, f"halo {cfg} conv {B}x{H}x{cin}->{cout}: {err:.3e}"
+
+
+@pytest.mark.parametrize("cfg", ["128,s", "256,s", "256,a"])
+@pytest.mark.parametrize("B,H,cin,cout", [(8, 7, 512, 512), (2, 14, 256, 256)])
+def test_conv_halo_candidates_fp16(ops, halo_cfg, cfg, B, H, cin, cout):
+    g = torch.Generator().manual_seed(B * 7 + H + cin)
+    x = torch.rand(B, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    x_in = x.permute(0, 2, 3, 1).contiguous().half()
+    ref = F.relu(F.conv2d(x_in.float().permute(0, 3, 1, 2), w.half().float(), None, 1, 1)).permute(0, 2, 3, 1)
+    wp = ops.pack_weight("fp16", ops.conv_weight_matrix(w, cin))
+    halo_cfg(cfg)
+    out = ops.conv2d("fp16", x_in.cuda(), wp, cout, 3, 3, 1, 1, act="relu")
+    err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
+    assert err < 2e-3, f"fp16 halo {cfg} conv {B}x{H}x{cin}->{cout}: {err:.3e}"

@@ -19,5 +19,5 @@ else
   mv "$tmp/starpu-inference-server_amd/csrc/"* "$tmp/pkg/csrc/"
 fi
 sed -i 's#-I../../include#-I../../include '"$*"'#' "$tmp/pkg/csrc/Makefile"
-make -s -C "$tmp/pkg/csrc" -j8 OUT="$out" >/dev/null
+make -s -C "$tmp/pkg/csrc" -j8 OUT="$out" "$out" >/dev/null
 echo "built $out ($rev ${*:-})"

@@ -65,14 +65,22 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--plans", default="", help="';'-separated SPI_GEMM_PLAN values to sweep ('' = the chooser)")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--halo-cfgs", default="", help="';'-separated SPI_GEMM_HALO_CFG values to sweep ('' = the chooser)")
+    ap.add_argument("--batch", type=int, default=0, help="override the conv batch (ResNet-152 bs32: 32)")
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
     plans = a.plans.split(";") if a.plans else [""]
+    if a.halo_cfgs:
+        plans = [("halo", c) for c in a.halo_cfgs.split(";")]
 
     def sweep(fn, label, fl):
         for plan in plans:
-            os.environ["SPI_GEMM_PLAN"] = plan
+            if isinstance(plan, tuple):
+                os.environ["SPI_GEMM_HALO_CFG"] = plan[1]
+                plan = "halo " + plan[1]
+            else:
+                os.environ["SPI_GEMM_PLAN"] = plan
             ops.lib.spi_debug_gemm_reload_env()  # knobs are cached in the library
             try:
                 ms = timeit(fn, a.reps)
@@ -81,6 +89,7 @@ def main():
                 continue
             print(f"{label}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s  [{plan or 'auto'}]", flush=True)
         os.environ["SPI_GEMM_PLAN"] = ""
+        os.environ["SPI_GEMM_HALO_CFG"] = ""
         ops.lib.spi_debug_gemm_reload_env()
     dt = ops.act_dtype(a.prec)
     ws = ops.workspace()
@@ -88,6 +97,7 @@ def main():
     for name, B, H, cin, cout, k, st in CONVS:
         if a.only and a.only not in name:
             continue
+        B = a.batch or B
         x = torch.randn(B, H, H, cin, device="cuda").to(dt)
         w = rng.standard_normal((cout, k * k * cin)).astype(np.float32) * 0.05
         wp = ops.pack_weight(a.prec, w)
