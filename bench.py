@@ -216,34 +216,45 @@ def committed_profile(kind, model, batch, precision):
         return json.load(f).get("ops", {}), os.path.relpath(hits[-1], ROOT)
 
 
-def roofline(h, precision, model):
-    """The dominant op under the four-stream load (largest device time per forward), its
-    algorithmic FLOPs per launch over its mean launch duration; the same op isolated beside it."""
-    loaded = h.op_profile(True)
-    iso = h.op_profile(False)
-    name, (tot, cnt, flops, nbytes) = max(loaded.items(), key=lambda kv: kv[1][0])
-    ms = tot / max(cnt, 1)
-    ms_iso = iso[name][0] / max(iso[name][1], 1)
-    fwd_ms = sum(v[0] for v in iso.values())
-    fwd_flops = sum(v[2] * v[1] for v in iso.values())
+def roofline(h, precision, model, reps=200, name=None):
+    """The dominant op under the four-stream load (largest device time per forward; `name`
+    overrides the choice), and its roofline: algorithmic FLOPs (or bytes) per launch over its
+    steady-state launch duration -- `reps` launches of that op back to back on worker 0's
+    stream between one pair of hipEvents (Model::profile_op), the same launches a rocprofv3
+    kernel trace of `bench.py --roofline-only --roofline-op NAME` counts (profiles/<round>/).
+    The per-launch event times under the four-stream load are reported beside it."""
+    loaded = h.op_profile(True) if name is None else None
+    if name is None:
+        name = max(loaded.items(), key=lambda kv: kv[1][0])[0]
+    micro = h.replica.profile_op(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream, name, reps)
+    ms, flops, nbytes = micro["ms"], micro["flops"], micro["bytes"]
     peak = PEAK_TFLOPS[precision]
     traffic, tsrc = committed_profile("traffic", model, h.batch, precision)
     mfma, msrc = committed_profile("mfma", model, h.batch, precision)
-    common = {"kernel": name, "launches_per_forward": cnt, "avg_launch_ms": round(ms, 5),
-              "avg_launch_ms_isolated": round(ms_iso, 5),
-              "forward_share_loaded": round(tot / sum(v[0] for v in loaded.values()), 4),
-              "traffic": traffic.get(name, {}).get("hbm_bytes_per_launch"), "traffic_source": tsrc,
-              "mfma_busy_pct": mfma.get(name, {}).get("mfma_busy_pct"), "mfma_source": msrc,
-              "isolated_forward_frac": round(fwd_flops / (fwd_ms * 1e-3) / 1e12 / peak, 5),
-              "measured": "hipEvents on the launch stream, 5 forwards under the 4-stream load / isolated"}
+    t_bytes = traffic.get(name, {}).get("hbm_bytes_per_launch")
+    common = {"kernel": name, "avg_launch_ms": round(ms, 5), "reps": reps,
+              "measured": f"hipEvents around {reps} back-to-back launches of the op on its stream "
+                          "(Model::profile_op); rocprofv3 summary of the same launches in profiles/",
+              "traffic": t_bytes, "traffic_source": tsrc,
+              "hbm_gbs": round(t_bytes / (ms * 1e-3) / 1e9, 1) if t_bytes else None,
+              "mfma_busy_pct": mfma.get(name, {}).get("mfma_busy_pct"), "mfma_source": msrc}
+    if loaded is not None:
+        tot, cnt = loaded[name][0], loaded[name][1]
+        fwd_loaded = sum(v[0] for v in loaded.values())
+        ms_l = tot / max(cnt, 1)
+        common["under_load"] = {
+            "launches_per_forward": cnt, "avg_launch_ms": round(ms_l, 5),
+            "forward_share": round(tot / fwd_loaded, 4),
+            "frac": round((flops / (ms_l * 1e-3) / 1e12 / peak) if flops else
+                          (nbytes / (ms_l * 1e-3) / 1e9 / PEAK_HBM_GBS), 5),
+            "measured": "hipEvents around each launch of one eager forward on worker 0 while the other "
+                        "workers replay forwards (5 forwards)"}
     if flops == 0:
         ach = nbytes / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(ach / PEAK_HBM_GBS, 5), "algorithmic_bytes_per_launch": nbytes,
-                "frac_isolated": round(nbytes / (ms_iso * 1e-3) / 1e9 / PEAK_HBM_GBS, 5), **common}
+                "frac": round(ach / PEAK_HBM_GBS, 5), "algorithmic_bytes_per_launch": nbytes, **common}
     ach = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 5),
-            "frac_isolated": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 5),
             "algorithmic_flops_per_launch": flops, "mfma_issue_per_flop": 3 if precision == "fp16x3" else 1,
             **common}
 
@@ -357,6 +368,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline budget per layout (0 = skip)")
     ap.add_argument("--e2e-requests", type=int, default=4000)
     ap.add_argument("--extras", type=int, default=1, help="single-GPU extra measurements (0 = skip)")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the dominant op's back-to-back launches (the rocprofv3 roofline command)")
+    ap.add_argument("--roofline-op", default="", help="op name for --roofline-only (default: chosen under load)")
+    ap.add_argument("--roofline-reps", type=int, default=200)
     args = ap.parse_args()
     # One HIP hardware queue per stream: HIP maps streams onto GPU_MAX_HW_QUEUES queues
     # round-robin (default 4, shared with torch's own streams), and streams that share a queue
@@ -389,6 +404,14 @@ def main():
     replica = spi.ModelReplica(model, dev, args.precision, max_batch=args.batch,
                                seq_len=seq if args.model.startswith("bert") else 0, graphs=bool(args.graphs))
     h = Harness(spi, replica, args.model, dev, args.batch, args.workers, np.random.default_rng(rank))
+    if args.roofline_only:
+        h.rounds(1)
+        torch.cuda.synchronize(dev)
+        rl = roofline(h, args.precision, args.model, args.roofline_reps, args.roofline_op or None)
+        if rank == 0:
+            print(json.dumps({"roofline_only": True, "config": WORKLOADS[args.model], "batch": args.batch,
+                              "dtype": args.precision, "roofline": rl}), flush=True)
+        return
     elapsed = h.throughput(args.steps, args.warmup, args.tasks_per_step, world, dist)
     per_step = args.workers * args.tasks_per_step * args.batch
     value = world * per_step * args.steps / elapsed
@@ -427,7 +450,7 @@ def main():
     if rank == 0:
         result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
         result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
-        result["roofline"] = roofline(h, args.precision, args.model)
+        result["roofline"] = roofline(h, args.precision, args.model, args.roofline_reps)
     if rank == 0 and world == 1:
         # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
         e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=4 * args.workers,

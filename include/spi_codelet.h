@@ -282,6 +282,13 @@ int spi_model_profile(spi_model* model, void* stream, int64_t batch, int64_t seq
                       const void* const* inputs, void* const* outputs, float* op_ms,
                       double* op_flops, double* op_bytes, char* op_names, int32_t name_len,
                       int32_t max_ops);
+/* Measurement hook: the same eager forward with the op named `op_name` (its
+ * first occurrence) launched `reps` times back to back between one pair of
+ * hipEvents; returns its device milliseconds per launch and its algorithmic
+ * FLOPs / HBM bytes per launch.  Returns 0, or -1 (unknown op, bad arguments). */
+int spi_model_profile_op(spi_model* model, void* stream, int64_t batch, int64_t seq,
+                         const void* const* inputs, void* const* outputs, const char* op_name,
+                         int32_t reps, float* ms_per_launch, double* flops, double* bytes);
 /* Capture launch-bound forwards into hipGraphs (per stream, per batch). */
 void spi_model_set_graphs(spi_model* model, int32_t enable);
 /* Per-worker warm-up (inference_runner.cpp:507-560): allocate `stream`'s

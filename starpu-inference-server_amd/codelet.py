@@ -234,6 +234,20 @@ class ModelReplica:
         return [dict(name=raw[i * name_len:(i + 1) * name_len].split(b"\0")[0].decode(), ms=ms[i], flops=fl[i],
                      bytes=by[i]) for i in range(n)]
 
+    def profile_op(self, inputs: Sequence[torch.Tensor], out: torch.Tensor, stream: int, name: str,
+                   reps: int = 200) -> dict:
+        """One eager forward with op `name` launched `reps` times back to back between one pair
+        of hipEvents on `stream`: its device time per launch (measurement only)."""
+        ins = (C.c_void_p * max(1, len(inputs)))(*[x.data_ptr() for x in inputs])
+        outs = (C.c_void_p * 1)(out.data_ptr())
+        ms, fl, by = C.c_float(), C.c_double(), C.c_double()
+        seq = int(inputs[0].shape[1]) if inputs[0].dim() >= 2 else 0
+        rc = lib.spi_model_profile_op(self.handle, C.c_void_p(stream), int(inputs[0].shape[0]), seq, ins, outs,
+                                      name.encode(), int(reps), C.byref(ms), C.byref(fl), C.byref(by))
+        if rc != 0:
+            raise InferenceExecutionException(f"profile_op failed: {N.last_error()}")
+        return dict(name=name, ms=ms.value, flops=fl.value, bytes=by.value, reps=reps)
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             lib.spi_model_destroy(self.handle)

@@ -373,6 +373,19 @@ int spi_model_profile(spi_model* m, void* stream, int64_t batch, int64_t seq, co
   }
 }
 
+int spi_model_profile_op(spi_model* m, void* stream, int64_t batch, int64_t seq, const void* const* inputs,
+                         void* const* outputs, const char* op_name, int32_t reps, float* ms, double* flops,
+                         double* bytes) {
+  if (!m) return -1;
+  try {
+    return m->impl->profile_op(static_cast<hipStream_t>(stream), (int)batch, (int)seq, inputs, outputs, op_name,
+                               (int)reps, ms, flops, bytes);
+  } catch (const std::exception& e) {
+    tl_last_error = e.what();
+    return -1;
+  }
+}
+
 void spi_model_set_graphs(spi_model* m, int32_t on) {
   if (m) m->impl->set_graphs(on != 0);
 }

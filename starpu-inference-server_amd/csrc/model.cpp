@@ -616,8 +616,7 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   d.out_split = split_;
   d.a_split = split_ && &c != &stem_;  // the stem reads the ingested fp32 image
   const size_t es = f16_ ? 2 : 4;
-  if (prof_)
-    op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
+  const int nrep = !prof_ ? 1 : op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
                     std::to_string(c.cout) + "_s" + std::to_string(c.stride) + "_M" + std::to_string(d.M),
              2.0 * d.M * d.N * (double)c.kh * c.kw * c.cin,
              (double)B * H * W * c.cin_pad * es + (double)c.cout * d.K * es + (double)d.M * d.N * es * (res ? 2 : 1));
@@ -632,7 +631,7 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
   if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
-  gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
   if (prof_) op_end(s);
 }
 
@@ -645,8 +644,7 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   d.ldr = ldr;
   d.wplane = L.wplane;
   const size_t es = f16_ ? 2 : 4;
-  if (prof_)
-    op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
+  const int nrep = !prof_ ? 1 : op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
              2.0 * M * L.n * (double)L.k,
              (double)M * L.k * es + (double)L.n * L.k * es + (double)M * L.n * (out_f32 ? 4 : es) +
                  (res ? (double)M * L.n * (res_f32 ? 4 : es) : 0.0));
@@ -661,7 +659,7 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
   if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
-  gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
   if (prof_) op_end(s);
 }
 
@@ -677,8 +675,7 @@ void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& 
   d.a_split = split_;
   d.wplane = fc_.wplane;
   const size_t es = f16_ ? 2 : 4;
-  if (prof_)
-    op_begin(s, "avgpool_fc_M" + std::to_string(B * hw) + "_N" + std::to_string(classes_) + "_K" +
+  const int nrep = !prof_ ? 1 : op_begin(s, "avgpool_fc_M" + std::to_string(B * hw) + "_N" + std::to_string(classes_) + "_K" +
                     std::to_string(feat_),
              2.0 * B * classes_ * (double)feat_,
              (double)B * hw * feat_ * es + (double)fc_.n * fc_.k * es + (double)B * classes_ * 4);
@@ -690,7 +687,7 @@ void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& 
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;
-  gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
   if (prof_) op_end(s);
 }
 
@@ -790,8 +787,9 @@ Workspace* Model::workspace(hipStream_t s) {
 // ---------------------------------------------------------------------------
 void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
-    if (prof_) op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);
-    ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
+    const int nrep = !prof_ ? 1 : op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);
+    for (int r = 0; r < nrep; ++r)
+      ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const double T = (double)B * S;
@@ -817,11 +815,13 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w, s);
     H = OH;
     const int PH = (H + 2 - 3) / 2 + 1;
-    if (prof_) op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
-    if (split_)
-      maxpool_nhwc_split(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, s);
-    else
-      maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    const int nrep = !prof_ ? 1 : op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
+    for (int r = 0; r < nrep; ++r) {
+      if (split_)
+        maxpool_nhwc_split(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, s);
+      else
+        maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    }
     if (prof_) op_end(s);
     H = PH;
     int cur = 2;
@@ -862,11 +862,13 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     w.final_buf = cur;
     w.final_hw = H * H;
     if (!pooled_fc(H * H)) {  // else avgpool + fc run as one GEMM in the epilogue
-      if (prof_) op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
-      if (split_)
-        avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
-      else
-        avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+      const int nrep = !prof_ ? 1 : op_begin(s, "avgpool", 0, (double)B * H * H * feat_ * (f16_ ? 2 : 4));
+      for (int r = 0; r < nrep; ++r) {
+        if (split_)
+          avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
+        else
+          avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+      }
       if (prof_) op_end(s);
       w.final_buf = 6;
     }
@@ -882,8 +884,10 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     for (int i = 0; i < layers_; ++i) {
       const TfLayer& L = tf_[i];
       run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s);
-      if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
-      attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
+      const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
+                                             (double)T * 4 * D_ * (f16_ ? 2 : 4));
+      for (int r = 0; r < nrep; ++r)
+        attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
       run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s);
       prof_op(s, "layernorm", ln_bytes(T, true), [&] {
@@ -913,8 +917,9 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
                   f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
       });
       run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s);
-      if (prof_) op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_, (double)T * 4 * D_ * (f16_ ? 2 : 4));
-      attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
+      const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
+                                             (double)T * 4 * D_ * (f16_ ? 2 : 4));
+      for (int r = 0; r < nrep; ++r) attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
       if (prof_) op_end(s);
       run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s);
       prof_op(s, "layernorm", ln_bytes(T, false), [&] {
@@ -1013,13 +1018,19 @@ void Model::warmup(hipStream_t s, int B, int S, bool mask) {
 namespace spi {
 
 thread_local std::vector<Model::OpRecord>* Model::prof_ = nullptr;
+thread_local Model::ProfRepeat* Model::prof_rep_ = nullptr;
 
-void Model::op_begin(hipStream_t s, const std::string& name, double flops, double bytes) {
-  OpRecord r{name, flops, bytes, nullptr, nullptr};
+int Model::op_begin(hipStream_t s, const std::string& name, double flops, double bytes) {
+  OpRecord r{name, flops, bytes, nullptr, nullptr, 1};
+  if (prof_rep_ && !prof_rep_->done && name == prof_rep_->name) {  // the op profile_op() repeats
+    prof_rep_->done = true;
+    r.reps = prof_rep_->reps;
+  }
   SPI_HIP(hipEventCreate(&r.start));
   SPI_HIP(hipEventCreate(&r.stop));
   SPI_HIP(hipEventRecord(r.start, s));
   prof_->push_back(r);
+  return r.reps;
 }
 
 void Model::op_end(hipStream_t s) { SPI_HIP(hipEventRecord(prof_->back().stop, s)); }
@@ -1046,7 +1057,7 @@ int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* con
     if (n < max_ops) {
       float t = 0.f;
       SPI_HIP(hipEventElapsedTime(&t, r.start, r.stop));
-      if (ms) ms[n] = t;
+      if (ms) ms[n] = t / r.reps;  // per launch
       if (flops) flops[n] = r.flops;
       if (bytes) bytes[n] = r.bytes;
       if (names && name_len > 0) std::snprintf(names + (size_t)n * name_len, name_len, "%s", r.name.c_str());
@@ -1056,6 +1067,40 @@ int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* con
     (void)hipEventDestroy(r.stop);
   }
   return n;
+}
+
+}  // namespace spi
+
+namespace spi {
+
+// One eager forward with op `name` (its first occurrence) launched `reps` times
+// back to back between one pair of events: its steady-state device time per
+// launch, without the event overhead of a single bracketed launch (bench.py's
+// roofline; the same launches a rocprofv3 kernel trace of that command counts).
+int Model::profile_op(hipStream_t s, int B, int S, const void* const* in, void* const* out, const char* name,
+                      int reps, float* ms, double* flops, double* bytes) {
+  if (!name || reps < 1) throw std::runtime_error("profile_op: name and reps >= 1 required");
+  ProfRepeat rep{name, reps, false};
+  prof_rep_ = &rep;
+  std::vector<float> t(4096);
+  std::vector<double> f(4096), b(4096);
+  std::vector<char> names((size_t)4096 * 96);
+  int n = 0;
+  try {
+    n = profile(s, B, S, in, out, t.data(), f.data(), b.data(), names.data(), 96, 4096);
+  } catch (...) {
+    prof_rep_ = nullptr;
+    throw;
+  }
+  prof_rep_ = nullptr;
+  for (int i = 0; i < n; ++i)
+    if (std::strcmp(names.data() + (size_t)i * 96, name) == 0) {
+      if (ms) *ms = t[i];
+      if (flops) *flops = f[i];
+      if (bytes) *bytes = b[i];
+      return 0;
+    }
+  throw std::runtime_error(std::string("profile_op: no op named ") + name);
 }
 
 }  // namespace spi

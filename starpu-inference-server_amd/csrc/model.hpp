@@ -81,9 +81,13 @@ class Model {
     double flops;
     double bytes;
     hipEvent_t start, stop;
+    int reps;  // launches between start and stop (profile_op)
   };
   int profile(hipStream_t s, int batch, int S, const void* const* in, void* const* out, float* ms,
               double* flops, double* bytes, char* names, int name_len, int max_ops);
+  // The same forward with op `name` launched `reps` times back to back; its time per launch.
+  int profile_op(hipStream_t s, int batch, int S, const void* const* in, void* const* out, const char* name,
+                 int reps, float* ms, double* flops, double* bytes);
 
   // Output element count per sample (for size checks).
   size_t out_elems_per_sample() const;
@@ -153,13 +157,21 @@ class Model {
   // Set only inside profile(), on the profiling thread: forwards running on
   // other worker threads at the same time never see it.
   static thread_local std::vector<OpRecord>* prof_;
-  void op_begin(hipStream_t s, const std::string& name, double flops, double bytes);
+  struct ProfRepeat {
+    std::string name;
+    int reps;
+    bool done;
+  };
+  static thread_local ProfRepeat* prof_rep_;
+  // Starts an op record; returns how many times the op is to be launched (1, or
+  // profile_op's repeat count for the op it names).
+  int op_begin(hipStream_t s, const std::string& name, double flops, double bytes);
   void op_end(hipStream_t s);
   // Profiled launch (bytes = algorithmic traffic); a plain call when not profiling.
   template <typename F>
   void prof_op(hipStream_t s, const char* name, double bytes, F&& launch) {
-    if (prof_) op_begin(s, name, 0, bytes);
-    launch();
+    const int nrep = prof_ ? op_begin(s, name, 0, bytes) : 1;
+    for (int r = 0; r < nrep; ++r) launch();
     if (prof_) op_end(s);
   }
   // LayerNorm over rows x D_: fp32 in + fp32 out (+ compute-type copy).
