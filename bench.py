@@ -2,8 +2,10 @@
 """MI355X inference-codelet benchmark (BASELINE.json metric: inferences/sec + p50 latency).
 
 Headline workload = BASELINE.json configs[1]: ResNet-18, batch 8 per task, fp16 MFMA, one
-MI355X -- run in the parity-grade fp16x3 mode (split-fp16 MFMA, fp32-grade results; plain fp16
-operands miss the 1e-3 bar on this network).  The `--workers` HIP worker streams
+MI355X -- run in the fp16m mode: fp16 activations and fp16 MFMA operands, with the layers that
+set the fp16 error (stem, downsample convs, FC) on split-fp16 weights; it holds the north_star
+1e-3 bar at this config (plain fp16 operands alone miss it on this random-init network,
+DESIGN.md 3.2).  The fp32-grade fp16x3 mode is reported beside it.  The `--workers` HIP worker streams
 of a GPU (STARPU_NWORKER_PER_CUDA=4, models/resnet18.yml:6) each call the HIP codelet
 (libspi_hip.so, through the C-ABI) on a synthetic batch already resident in HBM.  A *step* is
 `--tasks-per-step` codelet calls on every worker stream (default 8: 32 tasks = 256 images per GPU).
@@ -50,9 +52,13 @@ WORKLOADS = {
     "resnet152": "ResNet-152 bs=32 fp16, HIP workers per MI355X (request-parallel, no RCCL)",
     "vit_l_16": "ViT-L/16 224^2 bs=16 fp16 (patch-embed GEMM + MFMA attention, LDS-tiled)",
 }
-PEAK_TFLOPS = {"fp16": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"fp16": 2500.0, "fp16m": 2500.0, "fp16x3": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 PROFILE_ROUND = "r02"
+# The fp16 configs' parity-grade modes (north_star 1e-3): fp16m holds it on ResNet-18 at 224,
+# the deep bottleneck ResNet-152 needs fp16x3 (fp16m emulates at 6-7e-3), the transformers
+# pass in plain fp16 (fp32 softmax / LayerNorm / residual stream).
+DEFAULT_PRECISION = {"resnet18": "fp16m", "resnet152": "fp16x3", "bert_base": "fp16", "vit_l_16": "fp16"}
 
 
 def percentile(samples, p):
@@ -361,7 +367,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet18", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--precision", default="fp16x3", choices=["fp16", "fp16x3", "fp32"])
+    ap.add_argument("--precision", default=None, choices=["fp16", "fp16m", "fp16x3", "fp32"],
+                    help="default: the parity-grade fp16 mode of the model (DEFAULT_PRECISION)")
     ap.add_argument("--workers", type=int, default=4, help="worker streams per GPU")
     ap.add_argument("--tasks-per-step", type=int, default=8, help="codelet calls per worker per step")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
@@ -373,6 +380,7 @@ def main():
     ap.add_argument("--roofline-op", default="", help="op name for --roofline-only (default: chosen under load)")
     ap.add_argument("--roofline-reps", type=int, default=200)
     args = ap.parse_args()
+    args.precision = args.precision or DEFAULT_PRECISION[args.model]
     # One HIP hardware queue per stream: HIP maps streams onto GPU_MAX_HW_QUEUES queues
     # round-robin (default 4, shared with torch's own streams), and streams that share a queue
     # run serially -- 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues.  Room for the
@@ -438,6 +446,8 @@ def main():
             "step": f"{args.tasks_per_step} codelet calls on each of the {args.workers} worker streams "
                     f"({per_step} inferences per GPU)",
             "precision_mode": {"fp16x3": "split-fp16 MFMA (hi/lo fp16 operands, fp32 accumulate): fp32-grade parity",
+                               "fp16m": "fp16 MFMA operands + fp16 activations, fp32 accumulate; stem / downsample / "
+                                        "FC on split-fp16 weights (normalised max error 0.5-0.6e-3 at this config)",
                                "fp16": "fp16 MFMA operands, fp32 accumulate", "fp32": "fp32 MFMA"}[args.precision],
             "inputs": "resident in HBM (device-resident codelet rate; the PCIe-inclusive serving rate is `e2e`)",
             "graphs": bool(args.graphs),
@@ -466,14 +476,18 @@ def main():
 
     if rank == 0 and world == 1 and args.extras and args.model == "resnet18":
         extras = {}
-        # plain fp16 operands on the same workload (faster; 1.0e-3 .. 2.4e-3 parity on these networks)
-        r16 = spi.ModelReplica(model, dev, "fp16", max_batch=args.batch, graphs=True)
-        h16 = Harness(spi, r16, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
-        el = h16.throughput(args.steps, 2, args.tasks_per_step)
-        extras["resnet18_bs8_fp16_plain"] = {
-            "value": round(per_step * args.steps / el, 2), "unit": "inferences/s",
-            "parity_normalised_max_err": 1.0e-3, "note": "not parity-grade on ResNet: never the C2 figure"}
-        del r16, h16
+        # the same workload in the other modes: fp16x3 (fp32-grade, ~2e-6) and plain fp16
+        # operands everywhere (1.8e-3 .. 2.0e-3: misses the 1e-3 bar, never the C2 figure)
+        for prec in [p for p in ("fp16x3", "fp16") if p != args.precision]:
+            rp = spi.ModelReplica(model, dev, prec, max_batch=args.batch, graphs=True)
+            hp = Harness(spi, rp, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
+            el = hp.throughput(args.steps, 2, args.tasks_per_step)
+            extras[f"resnet18_bs8_{prec}"] = {
+                "value": round(per_step * args.steps / el, 2), "unit": "inferences/s",
+                "p50_task_latency_ms": round(percentile(hp.loaded_latency(10), 50), 4),
+                "parity": "fp32-grade (1.6e-6 .. 3.2e-6)" if prec == "fp16x3" else
+                          "1.8e-3 .. 2.0e-3 normalised max error: misses the 1e-3 bar, not a C2 result"}
+            del rp, hp
         # ResNet-18 bs=1 (the metric names it): device-resident tasks, and bs1 requests served
         r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
         h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2), h.streams)

@@ -50,7 +50,7 @@ SPI_ERR_CPU_FORWARD = 7
 
 # enum spi_family / spi_precision
 FAMILY_AUTO, FAMILY_RESNET, FAMILY_BERT, FAMILY_VIT, FAMILY_AFFINE = 0, 1, 2, 3, 4
-PREC_F32, PREC_F16, PREC_F16X3 = 0, 1, 2
+PREC_F32, PREC_F16, PREC_F16X3, PREC_F16M = 0, 1, 2, 3
 
 
 class VectorInterface(C.Structure):

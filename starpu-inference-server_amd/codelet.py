@@ -125,7 +125,7 @@ def load_model(path: str) -> torch.jit.ScriptModule:
 
 
 PRECISIONS = {"fp16": N.PREC_F16, "f16": N.PREC_F16, "fp32": N.PREC_F32, "f32": N.PREC_F32,
-              "fp16x3": N.PREC_F16X3, "f16x3": N.PREC_F16X3}
+              "fp16x3": N.PREC_F16X3, "f16x3": N.PREC_F16X3, "fp16m": N.PREC_F16M, "f16m": N.PREC_F16M}
 _FAMILIES = {None: N.FAMILY_AUTO, "auto": N.FAMILY_AUTO, "resnet": N.FAMILY_RESNET, "bert": N.FAMILY_BERT,
              "vit": N.FAMILY_VIT, "affine": N.FAMILY_AFFINE}
 

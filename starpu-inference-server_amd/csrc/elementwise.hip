@@ -163,8 +163,8 @@ __global__ __launch_bounds__(256) void avgpool_split_kernel(const _Float16* __re
 
 // Global average pool: one block per image; thread (g, c) sums pixels g, g+G, ...
 // of its 16-byte channel vector c, then the G partial sums meet in LDS.
-template <typename T>
-__global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, T* __restrict__ y,
+template <typename T, typename TO = T>
+__global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, TO* __restrict__ y,
                                                       int B, int HW, int C) {
   constexpr int VEC = 16 / (int)sizeof(T);
   __shared__ float part[256 * VEC];
@@ -186,14 +186,16 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, T
     for (int q = 0; q < VEC; ++q) part[threadIdx.x * VEC + q] = s[q];
     __syncthreads();
     if (threadIdx.x < CV) {
-      T o[VEC];
+      TO o[VEC];
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
         float t = 0.f;
         for (int gg = 0; gg < G; ++gg) t += part[(gg * CV + threadIdx.x) * VEC + q];
-        o[q] = cvt<T>(t / (float)HW);
+        o[q] = cvt<TO>(t / (float)HW);
       }
-      *reinterpret_cast<uint4*>(y + (size_t)b * C + threadIdx.x * VEC) = *reinterpret_cast<const uint4*>(o);
+#pragma unroll
+      for (int h = 0; h < (int)sizeof(o) / 16; ++h)
+        reinterpret_cast<uint4*>(y + (size_t)b * C + threadIdx.x * VEC)[h] = reinterpret_cast<const uint4*>(o)[h];
     }
   } else {
     for (int cv = threadIdx.x; cv < CV; cv += 256) {
@@ -204,10 +206,12 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, T
 #pragma unroll
         for (int q = 0; q < VEC; ++q) s[q] += static_cast<float>(e[q]);
       }
-      T o[VEC];
+      TO o[VEC];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) o[q] = cvt<T>(s[q] / (float)HW);
-      *reinterpret_cast<uint4*>(y + (size_t)b * C + cv * VEC) = *reinterpret_cast<const uint4*>(o);
+      for (int q = 0; q < VEC; ++q) o[q] = cvt<TO>(s[q] / (float)HW);
+#pragma unroll
+      for (int h = 0; h < (int)sizeof(o) / 16; ++h)
+        reinterpret_cast<uint4*>(y + (size_t)b * C + cv * VEC)[h] = reinterpret_cast<const uint4*>(o)[h];
     }
   }
 }
@@ -436,8 +440,11 @@ void avgpool_nhwc_split(const void* x, float* y, int B, int HW, int C, hipStream
   hipLaunchKernelGGL(avgpool_split_kernel, dim3(B), dim3(256), 0, s, (const _Float16*)x, y, HW, C);
 }
 
-void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s) {
-  if (f16)
+void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s, bool out_f32) {
+  if (f16 && out_f32)
+    hipLaunchKernelGGL((avgpool_kernel<_Float16, float>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
+                       (float*)y, B, HW, C);
+  else if (f16)
     hipLaunchKernelGGL((avgpool_kernel<_Float16>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
                        (_Float16*)y, B, HW, C);
   else

@@ -614,7 +614,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
     constexpr int G = BN / 8, RSTEP = NT / G, ITEMS = BM / RSTEP;
     const int cg = tid % G, r0 = tid / G;
     const int nb = n0 + cg * 8;
-    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
+    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : d.out_f16 ? 0 : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
     // output row of tile row `row`, -1 when it is not stored
     auto row_m = [&](int row) -> int {
       if constexpr (HALO) {

@@ -117,8 +117,9 @@ size_t pack_vec(const float* v, int n) { return g_blob->add(v, (size_t)n * sizeo
 
 // Conv weight [Cout][Cin][KH][KW] (+ eval BN) -> folded [Npad][Kpad], k =
 // (kh*KW + kw)*cin_pad + c; bias' = beta - mean * gamma / sqrt(var + eps).
+// lo_part: pack w - fp16(w) of the folded weights, with a zero bias (ResBlock::ds_lo).
 ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
-                int cin_pad, Prec prec, float bn_eps) {
+                int cin_pad, Prec prec, float bn_eps, bool lo_part = false) {
   const spi_named_tensor* wt = need(p, wname + ".weight");
   if (wt->ndim != 4) throw std::runtime_error(wname + ".weight must be 4-D");
   ConvW c;
@@ -150,14 +151,16 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   const float* w = fdata(wt);
   const int cin = c.cin, kh = c.kh, kw = c.kw, cp = c.cin_pad;
   c.wplane = (size_t)c.npad * c.kpad;
+  c.prec = prec;
   c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, [&](int n, int k) -> float {
     const int cell = k / cp, ci = k % cp;
     if (ci >= cin) return 0.f;
     const int y = cell / kw, x = cell % kw;
-    return (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
+    const float v = (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
+    return lo_part ? v - static_cast<float>(static_cast<_Float16>(v)) : v;
   });
   std::vector<float> bias(c.cout);
-  for (int o = 0; o < c.cout; ++o) bias[o] = (float)shift[o];
+  for (int o = 0; o < c.cout; ++o) bias[o] = lo_part ? 0.f : (float)shift[o];
   c.b = pack_vec(bias.data(), c.cout);
   return c;
 }
@@ -169,6 +172,7 @@ LinearW pack_linear(const float* w, const float* b, int N, int K, Prec prec) {
   L.kpad = round_up(K, 64);
   L.npad = round_up(N, 128);
   L.wplane = (size_t)L.npad * L.kpad;
+  L.prec = prec;
   L.w = pack_matrix(N, K, L.npad, L.kpad, prec,
                     [&](int n, int k) { return w[(size_t)n * K + k]; });
   std::vector<float> zeros;
@@ -234,10 +238,14 @@ bool ends_with(const PMap& p, const std::string& anchor) {
 // Construction
 // ---------------------------------------------------------------------------
 Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* params, int n)
-    : device_(device), family_(cfg.family), prec_(cfg.precision == SPI_PREC_F16 ? Prec::F16 : cfg.precision == SPI_PREC_F16X3 ? Prec::F16X3 : Prec::F32),
-      f16_(cfg.precision == SPI_PREC_F16),
+    : device_(device), family_(cfg.family),
+      prec_(cfg.precision == SPI_PREC_F16 || cfg.precision == SPI_PREC_F16M ? Prec::F16
+            : cfg.precision == SPI_PREC_F16X3                               ? Prec::F16X3
+                                                                            : Prec::F32),
+      f16_(cfg.precision == SPI_PREC_F16 || cfg.precision == SPI_PREC_F16M),
       max_batch_(std::max(1, cfg.max_batch)) {
-  if (cfg.precision != SPI_PREC_F16 && cfg.precision != SPI_PREC_F32 && cfg.precision != SPI_PREC_F16X3)
+  if (cfg.precision != SPI_PREC_F16 && cfg.precision != SPI_PREC_F32 && cfg.precision != SPI_PREC_F16X3 &&
+      cfg.precision != SPI_PREC_F16M)
     throw std::runtime_error("unsupported precision");
   PMap p;
   for (int i = 0; i < n; ++i) {
@@ -259,6 +267,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     aff_shift_ = cfg.affine_shift;
     os << "affine(x*" << aff_scale_ << "+" << aff_shift_ << ") f32";
   } else if (family_ == SPI_FAMILY_RESNET) {
+    mixed_ = cfg.precision == SPI_PREC_F16M;
     if (cfg.image_size > 0) image_ = cfg.image_size;
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-5f;
     build_resnet(strip_prefix(p, "layer1.0.conv1.weight"));
@@ -281,7 +290,8 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
   } else {
     throw std::runtime_error("unsupported model family");
   }
-  os << (prec_ == Prec::F16 ? " f16" : prec_ == Prec::F16X3 ? " f16x3" : " f32") << " maxB" << max_batch_;
+  os << (mixed_ ? " f16m" : prec_ == Prec::F16 ? " f16" : prec_ == Prec::F16X3 ? " f16x3" : " f32") << " maxB"
+     << max_batch_;
   desc_ = os.str();
   g_blob = nullptr;
 
@@ -308,8 +318,12 @@ void Model::build_resnet(const PMap& p) {
   bottleneck_ = has(p, "layer1.0.conv3.weight");
   // Stem input channels padded to one 16-byte chunk per pixel: 4 fp32
   // (F32, and F16X3 whose A is fp32) or 8 fp16 (F16).
-  const int cin_pad = prec_ == Prec::F16 ? 8 : 4;
-  stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, prec_, eps_);
+  // SPI_PREC_F16M: the stem reads the fp32 image with split weights (F16X3) and
+  // writes fp16; the downsample convs carry hi + lo weights; the FC runs F16X3 on
+  // fp32 pooled features (these layers set the fp16 error).
+  const Prec stem_prec = mixed_ ? Prec::F16X3 : prec_;
+  const int cin_pad = stem_prec == Prec::F16 ? 8 : 4;
+  stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, stem_prec, eps_);
   if (stem_.kh != 7 || stem_.cin != 3) throw std::runtime_error("resnet stem must be 7x7 over 3 channels");
   for (int L = 1; L <= 4; ++L) {
     int nb = 0;
@@ -329,11 +343,14 @@ void Model::build_resnet(const PMap& p) {
         blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", 1, 0, prec_, eps_);
       }
       blk.has_ds = has(p, pre + "downsample.0.weight");
-      if (blk.has_ds) blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_);
+      if (blk.has_ds) {
+        blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_);
+        if (mixed_) blk.ds_lo = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_, true);
+      }
       blocks_.push_back(blk);
     }
   }
-  fc_ = pack_linear_named(p, "fc", prec_);
+  fc_ = pack_linear_named(p, "fc", mixed_ ? Prec::F16X3 : prec_);
   classes_ = fc_.n;
   feat_ = fc_.k;
   // Channel chain: every conv must read exactly the channels its producer
@@ -601,20 +618,23 @@ size_t Model::conv_partial(const ConvW& c, int B, int H, int W) const {
   int OH, OW;
   GemmDesc d = conv_desc(c, B, H, W, OH, OW);
   d.a_split = split_ && &c != &stem_;  // as run_conv: the plan (halo, split-K) depends on it
-  return gemm_partial_floats(d, prec_);
+  return gemm_partial_floats(d, c.prec);
 }
 
 size_t Model::linear_partial(const LinearW& L, int M) const {
-  return gemm_partial_floats(linear_desc(L, M, L.k, L.n), prec_);
+  return gemm_partial_floats(linear_desc(L, M, L.k, L.n), L.prec);
 }
 
 void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
-                     Act act, const void* res, Workspace& ws, hipStream_t s) {
+                     Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32, bool res_f32) {
   GemmDesc d = conv_desc(c, B, H, W, OH, OW);
   d.act = act;
   d.wplane = c.wplane;
   d.out_split = split_;
   d.a_split = split_ && &c != &stem_;  // the stem reads the ingested fp32 image
+  d.out_f32 = out_f32;
+  d.res_f32 = res_f32;
+  d.out_f16 = f16_ && c.prec == Prec::F16X3 && !out_f32;  // F16M stem: F16X3 contraction, fp16 activations
   const size_t es = f16_ ? 2 : 4;
   const int nrep = !prof_ ? 1 : op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
                     std::to_string(c.cout) + "_s" + std::to_string(c.stride) + "_M" + std::to_string(d.M),
@@ -629,9 +649,9 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
-  if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
+  if (gemm_partial_floats(d, c.prec) > ws.partial_floats || gemm_counter_slots(d, c.prec) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
-  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, c.prec, s);
   if (prof_) op_end(s);
 }
 
@@ -657,16 +677,16 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
-  if (gemm_partial_floats(d, prec_) > ws.partial_floats || gemm_counter_slots(d, prec_) > kCounterSlots)
+  if (gemm_partial_floats(d, L.prec) > ws.partial_floats || gemm_counter_slots(d, L.prec) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
-  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, L.prec, s);
   if (prof_) op_end(s);
 }
 
 // avgpool + fc as one GEMM over every pixel of the last stage with a
 // column-mean epilogue (GemmDesc::pool_rows): the split / fp16 / fp32 activation
 // is the A operand as is, so the pooled vector never goes through HBM.
-bool Model::pooled_fc(int hw) const { return hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
+bool Model::pooled_fc(int hw) const { return !mixed_ && hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
 
 void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s) {
   GemmDesc d = linear_desc(fc_, B * hw, feat_, classes_);
@@ -687,7 +707,7 @@ void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& 
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;
-  for (int r = 0; r < nrep; ++r) gemm(d, p, prec_, s);
+  for (int r = 0; r < nrep; ++r) gemm(d, p, fc_.prec, s);
   if (prof_) op_end(s);
 }
 
@@ -706,7 +726,9 @@ Workspace* Model::workspace(hipStream_t s) {
   std::vector<size_t> sizes;  // bytes per buffer
   if (family_ == SPI_FAMILY_RESNET) {
     const int cp = stem_.cin_pad;
-    sizes.push_back((size_t)B * image_ * image_ * cp * es);  // ingest
+    sizes.push_back((size_t)B * image_ * image_ * cp * (stem_.prec == Prec::F16 ? 2 : 4));  // ingest
+    // F16M: the downsample outputs (and their ds_lo partials) are fp32 in the same pool
+    const size_t ea = mixed_ ? 4 : es;
     int H = image_, OH, OW;
     size_t amax = 0;
     partial = std::max(partial, conv_partial(stem_, B, H, H));
@@ -732,13 +754,14 @@ Workspace* Model::workspace(hipStream_t s) {
       }
       if (b.has_ds) {
         partial = std::max(partial, conv_partial(b.ds, B, H, H));
+        if (mixed_) partial = std::max(partial, conv_partial(b.ds_lo, B, H, H));
         amax = std::max(amax, (size_t)B * H2 * H2 * b.ds.cout);
       }
       H = H2;
     }
     partial = std::max(partial, linear_partial(fc_, B));
-    for (int i = 0; i < 5; ++i) sizes.push_back(amax * es);
-    sizes.push_back((size_t)B * feat_ * es);  // pooled
+    for (int i = 0; i < 5; ++i) sizes.push_back(amax * ea);
+    sizes.push_back((size_t)B * feat_ * ea);  // pooled (fp32 under F16M: the FC's A)
   } else if (family_ == SPI_FAMILY_BERT) {
     const size_t T = (size_t)B * seq_;
     sizes = {T * D_ * 4, T * D_ * es, T * 3 * D_ * es, T * D_ * es, T * D_ * 4, T * ffn_ * es};
@@ -789,7 +812,8 @@ void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStrea
   if (family_ == SPI_FAMILY_RESNET) {
     const int nrep = !prof_ ? 1 : op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);
     for (int r = 0; r < nrep; ++r)
-      ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad, f16_, s);
+      ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad,
+                  stem_.prec == Prec::F16, s);
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const double T = (double)B * S;
@@ -838,23 +862,35 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         const int t2 = pick({cur, t1});
         run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
-        if (b.has_ds) {
+        if (b.has_ds && mixed_) {
+          const int lo = pick({cur, t2});
+          run_conv(b.ds_lo, buf[cur], B, H, H, buf[lo], OH, OW, Act::None, nullptr, w, s, true);
+          ident = pick({cur, t2, lo});
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, buf[lo], w, s, true, true);
+        } else if (b.has_ds) {
           ident = pick({cur, t2});
           run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
         }
         const int o = pick({cur, t2, ident});
-        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
+        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
+                 mixed_ && b.has_ds);
         cur = o;
       } else {
         const int t1 = pick({cur});
         run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
-        if (b.has_ds) {
+        if (b.has_ds && mixed_) {  // fp32 out = x . w_hi + bias + (x . w_lo)
+          const int lo = pick({cur, t1});
+          run_conv(b.ds_lo, buf[cur], B, H, H, buf[lo], OH, OW, Act::None, nullptr, w, s, true);
+          ident = pick({cur, t1, lo});
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, buf[lo], w, s, true, true);
+        } else if (b.has_ds) {
           ident = pick({cur, t1});
           run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
         }
         const int o = pick({cur, t1, ident});
-        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
+        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
+                 mixed_ && b.has_ds);
         cur = o;
       }
       H = H2;
@@ -867,7 +903,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         if (split_)
           avgpool_nhwc_split(buf[cur], static_cast<float*>(buf[6]), B, H * H, feat_, s);  // fp32 for the F16X3 FC
         else
-          avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s);
+          avgpool_nhwc(buf[cur], buf[6], B, H * H, feat_, f16_, s, mixed_);  // F16M: fp32 for the F16X3 FC
       }
       if (prof_) op_end(s);
       w.final_buf = 6;

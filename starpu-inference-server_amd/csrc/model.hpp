@@ -24,6 +24,7 @@ struct ConvW {
   int cout = 0, cin = 0, cin_pad = 0, kh = 1, kw = 1, stride = 1, pad = 0;
   int kpad = 0, npad = 0;
   size_t wplane = 0;
+  Prec prec = Prec::F16;  // packing / contraction precision of this conv
 };
 
 struct LinearW {
@@ -31,6 +32,7 @@ struct LinearW {
   int n = 0, k = 0, kpad = 0, npad = 0;
   size_t wplane = 0;
   bool has_bias = true;
+  Prec prec = Prec::F16;
 };
 
 struct LnW {
@@ -41,6 +43,10 @@ struct ResBlock {
   ConvW c1, c2, c3;  // c3 only for bottleneck
   bool has_ds = false;
   ConvW ds;
+  // SPI_PREC_F16M: the downsample's weights as hi (ds, fp16) + lo (ds_lo, fp16 of
+  // w - hi, no bias): ds_lo runs first into an fp32 buffer that ds adds as its
+  // residual, so the conv sees the weights to ~22 bits with plain fp16 MFMAs.
+  ConvW ds_lo;
 };
 
 struct TfLayer {  // BERT (post-LN) / ViT (pre-LN) encoder layer
@@ -107,7 +113,8 @@ class Model {
                 bool out_f32, Act act, const void* res, bool res_f32, int ldr, Workspace& ws,
                 hipStream_t s);
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
-                Act act, const void* res, Workspace& ws, hipStream_t s);
+                Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32 = false,
+                bool res_f32 = false);
   bool pooled_fc(int hw) const;
   void run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s);
   size_t conv_partial(const ConvW& c, int B, int H, int W) const;
@@ -121,6 +128,7 @@ class Model {
   int family_ = 0;
   Prec prec_ = Prec::F16;
   bool f16_ = true;  // activations stored as fp16 (Prec::F16 only)
+  bool mixed_ = false;  // SPI_PREC_F16M on a ResNet (ResBlock::ds_lo, stem / FC in F16X3)
   // ResNet under Prec::F16X3: conv outputs / pool inputs in the split layout
   // (GemmDesc::a_split), so the GEMM main loop never splits A on the VALU.
   bool split_ = false;

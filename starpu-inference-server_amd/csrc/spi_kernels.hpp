@@ -33,6 +33,7 @@ struct GemmDesc {
   int H = 0, W = 0, Cin = 0, OH = 0, OW = 0, KH = 1, KW = 1, stride = 1, pad = 0;
   Act act = Act::None;
   bool out_f32 = false;  // C is float (else the compute type)
+  bool out_f16 = false;  // C is fp16 although the mode's output type is fp32 (F16X3, plain stores)
   bool res_f32 = false;  // residual is float (else the compute type)
   // F16X3 activation split layout: per row, blocks of 32 elements stored as
   // [32 hi fp16 | 32 lo fp16] (128 bytes, the size of 32 fp32), hi = fp16(x),
@@ -74,7 +75,7 @@ void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH,
                   int OW, int k, int stride, int pad, bool f16, hipStream_t s);
 // Global average pool NHWC [B,HW,C] -> [B,C] (compute type).
 void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16,
-                  hipStream_t s);
+                  hipStream_t s, bool out_f32 = false);  // out_f32: fp16 in, fp32 out
 // The same two on F16X3 split activations (GemmDesc::a_split layout, C % 32 == 0):
 // max pool split -> split, average pool split -> fp32 [B,C].
 void maxpool_nhwc_split(const void* x, void* y, int B, int H, int W, int C, int OH,

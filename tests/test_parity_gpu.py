@@ -22,6 +22,12 @@ TOL = {"fp32": 1e-5, "fp16": 1e-3, "fp16x3": 1e-5}  # fp16x3 measures 1.6e-6 .. 
 # format's floor, not a kernel defect; fp16x3 (split-fp16 MFMA) is the
 # parity-grade fp16 mode and is held to the 1e-3 bar (it lands near 1e-6).
 TOL_RESNET_PLAIN_FP16 = 3e-3
+# fp16m (SPI_PREC_F16M): plain fp16 everywhere except the stem, the downsample convs and
+# the FC.  CPU emulation on ResNet-18 bs8@224: 0.48e-3 .. 0.60e-3 over
+# four input seeds (plain fp16 0.94e-3 .. 1.04e-3); held to the north_star 1e-3 bar.
+# Deep bottleneck nets amplify fp16 rounding (ResNet-152 emulated: fp16 11e-3, fp16m
+# 6-7e-3), so C4 is served in fp16x3 and fp16m is held to the plain-fp16 bound there.
+TOL_RESNET18_FP16M = 1e-3
 
 
 def hip_forward(spi, replica, inputs, out_shape, graphs=False):
@@ -39,11 +45,16 @@ def image(rng, b, size):
     return rng.random((b, 3, size, size), dtype=np.float32)
 
 
-def resnet_tol(prec):
+def resnet_tol(prec, at_config=True):
+    """at_config: ResNet-18 at the reference resolution (224), where fp16m is held to 1e-3.
+    The reduced 64x64 / bottleneck cases sit at 1.1e-3 in fp16m (emulated 1.06e-3: activation
+    rounding spread over every layer, no single layer dominates) and keep the plain-fp16 bound."""
+    if prec == "fp16m":
+        return TOL_RESNET18_FP16M if at_config else TOL_RESNET_PLAIN_FP16
     return TOL_RESNET_PLAIN_FP16 if prec == "fp16" else TOL[prec]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3", "fp16m"])
 def test_resnet18_small_image(spi, zoo, gpu, prec):
     rng = np.random.default_rng(0)
     m = zoo.resnet18(image=64)
@@ -54,11 +65,11 @@ def test_resnet18_small_image(spi, zoo, gpu, prec):
     err = normalized_max_error(got, ref)
     print(f"resnet18@64 {prec} err={err:.3e}")
     assert np.isfinite(got).all()
-    assert err < resnet_tol(prec)
+    assert err < resnet_tol(prec, at_config=False)
     assert top1_agreement(got, ref) == 1.0
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3", "fp16m"])
 def test_resnet_bottleneck_small(spi, zoo, gpu, prec):
     rng = np.random.default_rng(1)
     m = zoo.resnet([1, 2, 2, 1], True, image=64)
@@ -68,10 +79,10 @@ def test_resnet_bottleneck_small(spi, zoo, gpu, prec):
     got = hip_forward(spi, rep, [x], ref.shape)
     err = normalized_max_error(got, ref)
     print(f"resnet-bottleneck@64 {prec} err={err:.3e}")
-    assert err < resnet_tol(prec)
+    assert err < resnet_tol(prec, at_config=False)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16x3", "fp16m"])
 def test_resnet18_full_bs8(spi, zoo, gpu, prec):
     """C2: ResNet-18 bs=8 at 224x224."""
     rng = np.random.default_rng(2)
@@ -86,6 +97,20 @@ def test_resnet18_full_bs8(spi, zoo, gpu, prec):
     assert err < resnet_tol(prec)
     assert top1_agreement(got, ref) == 1.0
     np.testing.assert_array_equal(got, got_g)
+
+
+@pytest.mark.parametrize("seed", [3, 7, 11])
+def test_resnet18_fp16m_c2_seeds(spi, zoo, gpu, seed):
+    """C2 in the fp16m mode over more input draws (the 1e-3 bar, top-1 agreement)."""
+    m = zoo.resnet18()
+    x = image(np.random.default_rng(seed), 8, 224)
+    ref = cpu_inference(m, [x])[0]
+    rep = spi.ModelReplica(m, 0, "fp16m", max_batch=8)
+    got = hip_forward(spi, rep, [x], ref.shape, graphs=True)
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@224 bs8 fp16m seed{seed} err={err:.3e}")
+    assert err < TOL_RESNET18_FP16M
+    assert top1_agreement(got, ref) == 1.0
 
 
 def bert_inputs(rng, b, s, vocab=30522, pad_from=None):
