@@ -463,11 +463,17 @@ def main():
         result["roofline"] = roofline(h, args.precision, args.model, args.roofline_reps)
     if rank == 0 and world == 1:
         # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
-        e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=4 * args.workers,
+        # closed loop, 8 requests in flight per worker (the H2D link -- 51 GB/s measured, 85k inf/s of
+        # fp32 NCHW bs8 input -- and the compute pipeline both stay busy); and half that load
+        e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=8 * args.workers,
                           workers=args.workers)
         e2e["fraction_of_device_resident"] = round(e2e["value"] / value, 4)
         e2e["pipeline"] = "4 workers x depth 2, per-device copy stream, pinned slot pool of 8, 4 host copy threads"
         result["e2e"] = e2e
+        half = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=4 * args.workers,
+                           workers=args.workers)
+        result["e2e_half_load"] = {k: half[k] for k in ("value", "unit", "p50_latency_ms", "p95_latency_ms",
+                                                        "p99_latency_ms", "requests", "inflight")}
         e2e1 = h.serial_e2e(40)
         result["p50_serial_e2e_latency_ms"] = round(percentile(e2e1, 50), 4)
 

@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--precision", default="fp16x3")
+    ap.add_argument("--precision", default="fp16m")
     ap.add_argument("--requests", type=int, default=4000)
     ap.add_argument("--quick", type=int, default=0)
     args = ap.parse_args()
@@ -33,7 +33,7 @@ def main():
     x = np.random.default_rng(0).random((args.batch, 3, 224, 224), dtype=np.float32)
     import bench
     h = bench.Harness(spi, rep, args.model, 0, args.batch, 4, np.random.default_rng(1))
-    el, _ = h.throughput(200, 10)
+    el = h.throughput(200, 10)
     print(json.dumps({"device_resident_inf_per_s": round(4 * args.batch * 200 / el, 1),
                       "queues": os.environ["GPU_MAX_HW_QUEUES"]}), flush=True)
     del h
@@ -45,7 +45,8 @@ def main():
                     grid.append(dict(h2d_mode=h2d, pipeline_depth=depth, copy_threads=copy_threads,
                                      inflight=inflight))
     if args.quick:
-        grid = [g for g in grid if g["copy_threads"] == 4 and g["inflight"] == 16]
+        grid = [dict(h2d_mode=m, pipeline_depth=d, copy_threads=c, inflight=i) for m in ["device_stream", "worker_copy"]
+                for d in [2, 3] for c in [4, 8] for i in [16, 32]]
     for g in grid:
         inflight = g.pop("inflight")
         rt = rtmod.Runtime([rep], [((3, 224, 224), np.float32)], [(1000, np.float32)], max_batch=args.batch,
