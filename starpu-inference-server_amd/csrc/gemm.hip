@@ -465,10 +465,11 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   int cu_cell = 0, cu_kw = 0, cu_ci = 0, cu_off = 0;
   if constexpr (TAP) {
     {
-      cu_cell = kbeg >> a.cin_shift;
+      const int kbeg_a = kbeg / d.krep;  // A k of the slice's first step (slices hold whole krep groups)
+      cu_cell = kbeg_a >> a.cin_shift;
       const int kh = (cu_cell * a.kw_mul) >> 16;
       cu_kw = cu_cell - kh * d.KW;
-      cu_ci = kbeg & (d.Cin - 1);
+      cu_ci = kbeg_a & (d.Cin - 1);
       cu_off = ((kh * d.W + cu_kw) << a.cin_shift) + cu_ci;
     }
   }
@@ -495,15 +496,18 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
           SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
         }
         // advance one k-step: next channel block, or the next tap (next pixel,
-        // or the next filter row: W - KW + 1 pixels on)
-        cu_ci += ESTEP;
-        cu_off += ESTEP;
-        if (cu_ci == d.Cin) {
-          cu_ci = 0;
-          ++cu_cell;
-          if (++cu_kw == d.KW) {
-            cu_kw = 0;
-            cu_off += (d.W - d.KW) << a.cin_shift;
+        // or the next filter row: W - KW + 1 pixels on); krep = 2: after the
+        // second (lo-weight) step of the pair only
+        if (d.krep == 1 || (step & 1)) {
+          cu_ci += ESTEP;
+          cu_off += ESTEP;
+          if (cu_ci == d.Cin) {
+            cu_ci = 0;
+            ++cu_cell;
+            if (++cu_kw == d.KW) {
+              cu_kw = 0;
+              cu_off += (d.W - d.KW) << a.cin_shift;
+            }
           }
         }
       } else {
@@ -526,9 +530,11 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
         }
       }
     } else {
+      // krep = 2: packed steps 2s and 2s + 1 both stage A step s
+      const int ka0 = d.krep == 2 ? (k0 / (2 * ESTEP)) * ESTEP : k0;
 #pragma unroll
       for (int q = 0; q < AQ; ++q) {
-        const int k = k0 + a_koff[q];
+        const int k = ka0 + a_koff[q];
         const char* src = (a_ok[q] && k < d.K) ? reinterpret_cast<const char*>(a_pix[q] + k) : zeros;
         SPI_DMA_A((const void*)SPI_A_SRC(src), (lds_ptr_t)(dst + (wave * AQ + q) * 1024), 16, 0, 0);
       }
@@ -1159,13 +1165,14 @@ Knobs& knobs() {
   return k;
 }
 
-Plan finish_plan(Plan pl, int ksteps, int ES) {
+Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   const Knobs& k = knobs();
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
   if (pl.bm != 64 || pl.bn != 64) pl.splits = 1;  // split-K exists in the 64x64 kernels only
   if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
   pl.splits = std::max(1, std::min(pl.splits, ksteps));
-  const int kt = (ksteps + pl.splits - 1) / pl.splits;
+  int kt = (ksteps + pl.splits - 1) / pl.splits;
+  kt = (kt + krep - 1) / krep * krep;  // krep: slices hold whole (hi, lo) step pairs
   pl.k_per_split = kt * ES;
   pl.splits = (ksteps + kt - 1) / kt;
   return pl;
@@ -1220,7 +1227,7 @@ Plan halo_candidate(const GemmDesc& d, Prec prec, int T, int bm, bool stacked, i
 Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
   Plan no{};
   const int ES = estep_of(prec);
-  if (!knobs().halo || knobs().forced || !d.conv || d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 ||
+  if (!knobs().halo || knobs().forced || d.krep != 1 || !d.conv || d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 ||
       d.Cin < ES || d.Cin % ES || (prec == Prec::F16X3 && !d.a_split) || d.N % 64 || d.OH != d.H || d.OW != d.W)
     return no;
   if (knobs().halo_bm) return halo_candidate(d, prec, T, knobs().halo_bm, knobs().halo_stacked, 1 << 20);
@@ -1284,30 +1291,30 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   const Knobs& k = knobs();
   const int ES = estep_of(prec);
   const int ksteps = d.Kpad / ES;
-  if (k.forced) return finish_plan(k.plan, ksteps, ES);
+  if (k.forced) return finish_plan(k.plan, ksteps, ES, d.krep);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
   const auto stages_for = [](int kt) { return kt >= 16 ? 3 : 2; };  // a deeper ring pays only on long K loops
-  if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES);  // one image per tile row
+  if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);  // one image per tile row
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
     const int T = k.target;
-    if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES);
-    if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES);
+    if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
+    if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
     const int t64 = tiles_of(64, 64);
     const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
-    return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES);
+    return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
   }
   constexpr int kTarget = 256;  // CUs
-  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES);
+  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
   if (prec == Prec::F16 && tiles_of(128, 64) >= 384 && ksteps >= 32)
-    return finish_plan(Plan{128, 64, 3, 1, 0}, ksteps, ES);
+    return finish_plan(Plan{128, 64, 3, 1, 0}, ksteps, ES, d.krep);
   const int tiles = tiles_of(64, 64);
   int splits = 1;
   if (tiles < kTarget) {
     const int want = (prec == Prec::F16 ? 384 : 512) / tiles;  // workgroups per launch
     splits = std::max(1, std::min(want, ksteps / 6));            // >= 6 k-steps per slice
   }
-  return finish_plan(Plan{64, 64, stages_for((ksteps + splits - 1) / splits), splits, 0}, ksteps, ES);
+  return finish_plan(Plan{64, 64, stages_for((ksteps + splits - 1) / splits), splits, 0}, ksteps, ES, d.krep);
 }
 
 int ilog2(int v) {
@@ -1414,6 +1421,9 @@ extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   if (d.pool_rows && (d.conv || d.pool_rows > 64 || d.M % d.pool_rows))
     throw std::invalid_argument("pooled GEMM: dense A, pool_rows <= 64 dividing M");
+  if (d.krep != 1 && (d.krep != 2 || prec != Prec::F16 || d.Kpad % (2 * estep_of(prec)) ||
+                      (d.conv && (d.Cin < estep_of(prec) || d.KH * d.KW > 31))))
+    throw std::invalid_argument("krep = 2 needs F16, a packed Kpad of whole step pairs and dense or one-tap-per-step A");
   switch (prec) {
     case Prec::F16:
       launch<(int)Prec::F16>(d, p, s);

@@ -117,9 +117,10 @@ size_t pack_vec(const float* v, int n) { return g_blob->add(v, (size_t)n * sizeo
 
 // Conv weight [Cout][Cin][KH][KW] (+ eval BN) -> folded [Npad][Kpad], k =
 // (kh*KW + kw)*cin_pad + c; bias' = beta - mean * gamma / sqrt(var + eps).
-// lo_part: pack w - fp16(w) of the folded weights, with a zero bias (ResBlock::ds_lo).
+// hilo (F16 only): pack every 64-k block of the folded weights twice -- fp16(w), then
+// fp16(w - fp16(w)) -- for a krep = 2 contraction (GemmDesc::krep).
 ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
-                int cin_pad, Prec prec, float bn_eps, bool lo_part = false) {
+                int cin_pad, Prec prec, float bn_eps, bool hilo = false) {
   const spi_named_tensor* wt = need(p, wname + ".weight");
   if (wt->ndim != 4) throw std::runtime_error(wname + ".weight must be 4-D");
   ConvW c;
@@ -133,6 +134,7 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   const int K = c.kh * c.kw * c.cin_pad;
   c.kpad = round_up(K, 64);
   c.npad = round_up(c.cout, 128);
+  if (hilo && prec != Prec::F16) throw std::runtime_error("hi/lo weight packing is an F16 layout");
   std::vector<double> scale(c.cout, 1.0), shift(c.cout, 0.0);
   if (!bn.empty()) {
     const float* g = fdata(need(p, bn + ".weight"));
@@ -150,31 +152,53 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   }
   const float* w = fdata(wt);
   const int cin = c.cin, kh = c.kh, kw = c.kw, cp = c.cin_pad;
-  c.wplane = (size_t)c.npad * c.kpad;
   c.prec = prec;
-  c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, [&](int n, int k) -> float {
+  auto folded = [&](int n, int k) -> float {
     const int cell = k / cp, ci = k % cp;
     if (ci >= cin) return 0.f;
     const int y = cell / kw, x = cell % kw;
-    const float v = (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
-    return lo_part ? v - static_cast<float>(static_cast<_Float16>(v)) : v;
-  });
+    return (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
+  };
+  if (hilo) {
+    c.krep = 2;
+    c.kpad *= 2;
+    c.w = pack_matrix(c.cout, c.kpad, c.npad, c.kpad, prec, [&](int n, int kp) -> float {
+      const int k = (kp >> 7) * 64 + (kp & 63);  // 128-k packed block = [64 hi | 64 lo]
+      if (k >= K) return 0.f;
+      const float v = folded(n, k);
+      return (kp & 64) ? v - static_cast<float>(static_cast<_Float16>(v)) : v;
+    });
+  } else {
+    c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, folded);
+  }
+  c.wplane = (size_t)c.npad * c.kpad;
   std::vector<float> bias(c.cout);
-  for (int o = 0; o < c.cout; ++o) bias[o] = lo_part ? 0.f : (float)shift[o];
+  for (int o = 0; o < c.cout; ++o) bias[o] = (float)shift[o];
   c.b = pack_vec(bias.data(), c.cout);
   return c;
 }
 
-LinearW pack_linear(const float* w, const float* b, int N, int K, Prec prec) {
+LinearW pack_linear(const float* w, const float* b, int N, int K, Prec prec, bool hilo = false) {
   LinearW L;
   L.n = N;
   L.k = K;
   L.kpad = round_up(K, 64);
   L.npad = round_up(N, 128);
-  L.wplane = (size_t)L.npad * L.kpad;
   L.prec = prec;
-  L.w = pack_matrix(N, K, L.npad, L.kpad, prec,
-                    [&](int n, int k) { return w[(size_t)n * K + k]; });
+  if (hilo) {  // as pack_conv: [64 hi | 64 lo] per 64-k block, krep = 2
+    if (prec != Prec::F16) throw std::runtime_error("hi/lo weight packing is an F16 layout");
+    L.krep = 2;
+    L.kpad *= 2;
+    L.w = pack_matrix(N, L.kpad, L.npad, L.kpad, prec, [&](int n, int kp) -> float {
+      const int k = (kp >> 7) * 64 + (kp & 63);
+      if (k >= K) return 0.f;
+      const float v = w[(size_t)n * K + k];
+      return (kp & 64) ? v - static_cast<float>(static_cast<_Float16>(v)) : v;
+    });
+  } else {
+    L.w = pack_matrix(N, K, L.npad, L.kpad, prec, [&](int n, int k) { return w[(size_t)n * K + k]; });
+  }
+  L.wplane = (size_t)L.npad * L.kpad;
   std::vector<float> zeros;
   if (!b) {
     zeros.assign(N, 0.f);
@@ -185,11 +209,11 @@ LinearW pack_linear(const float* w, const float* b, int N, int K, Prec prec) {
   return L;
 }
 
-LinearW pack_linear_named(const PMap& p, const std::string& name, Prec prec) {
+LinearW pack_linear_named(const PMap& p, const std::string& name, Prec prec, bool hilo = false) {
   const spi_named_tensor* wt = need(p, name + ".weight");
   if (wt->ndim != 2) throw std::runtime_error(name + ".weight must be 2-D");
   const float* b = has(p, name + ".bias") ? fdata(need(p, name + ".bias")) : nullptr;
-  return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], prec);
+  return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], prec, hilo);
 }
 
 LnW pack_ln(const PMap& p, const std::string& name) {
@@ -319,8 +343,8 @@ void Model::build_resnet(const PMap& p) {
   // Stem input channels padded to one 16-byte chunk per pixel: 4 fp32
   // (F32, and F16X3 whose A is fp32) or 8 fp16 (F16).
   // SPI_PREC_F16M: the stem reads the fp32 image with split weights (F16X3) and
-  // writes fp16; the downsample convs carry hi + lo weights; the FC runs F16X3 on
-  // fp32 pooled features (these layers set the fp16 error).
+  // writes fp16; the downsample convs and the (avgpool-fused) FC carry hi + lo
+  // weights (krep = 2) (these layers set the fp16 error).
   const Prec stem_prec = mixed_ ? Prec::F16X3 : prec_;
   const int cin_pad = stem_prec == Prec::F16 ? 8 : 4;
   stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, stem_prec, eps_);
@@ -343,14 +367,11 @@ void Model::build_resnet(const PMap& p) {
         blk.c2 = pack_conv(p, pre + "conv2", pre + "bn2", 1, 0, prec_, eps_);
       }
       blk.has_ds = has(p, pre + "downsample.0.weight");
-      if (blk.has_ds) {
-        blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_);
-        if (mixed_) blk.ds_lo = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_, true);
-      }
+      if (blk.has_ds) blk.ds = pack_conv(p, pre + "downsample.0", pre + "downsample.1", s, 0, prec_, eps_, mixed_);
       blocks_.push_back(blk);
     }
   }
-  fc_ = pack_linear_named(p, "fc", mixed_ ? Prec::F16X3 : prec_);
+  fc_ = pack_linear_named(p, "fc", prec_, mixed_);
   classes_ = fc_.n;
   feat_ = fc_.k;
   // Channel chain: every conv must read exactly the channels its producer
@@ -598,6 +619,7 @@ GemmDesc conv_desc(const ConvW& c, int B, int H, int W, int& OH, int& OW) {
   d.KW = c.kw;
   d.stride = c.stride;
   d.pad = c.pad;
+  d.krep = c.krep;
   return d;
 }
 
@@ -610,6 +632,7 @@ GemmDesc linear_desc(const LinearW& L, int M, int lda, int ldc) {
   d.lda = lda;
   d.ldc = ldc;
   d.ldr = ldc;
+  d.krep = L.krep;
   return d;
 }
 }  // namespace
@@ -686,7 +709,7 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
 // avgpool + fc as one GEMM over every pixel of the last stage with a
 // column-mean epilogue (GemmDesc::pool_rows): the split / fp16 / fp32 activation
 // is the A operand as is, so the pooled vector never goes through HBM.
-bool Model::pooled_fc(int hw) const { return !mixed_ && hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
+bool Model::pooled_fc(int hw) const { return hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
 
 void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s) {
   GemmDesc d = linear_desc(fc_, B * hw, feat_, classes_);
@@ -727,7 +750,7 @@ Workspace* Model::workspace(hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
     const int cp = stem_.cin_pad;
     sizes.push_back((size_t)B * image_ * image_ * cp * (stem_.prec == Prec::F16 ? 2 : 4));  // ingest
-    // F16M: the downsample outputs (and their ds_lo partials) are fp32 in the same pool
+    // F16M: the downsample outputs are fp32 in the same pool
     const size_t ea = mixed_ ? 4 : es;
     int H = image_, OH, OW;
     size_t amax = 0;
@@ -754,7 +777,6 @@ Workspace* Model::workspace(hipStream_t s) {
       }
       if (b.has_ds) {
         partial = std::max(partial, conv_partial(b.ds, B, H, H));
-        if (mixed_) partial = std::max(partial, conv_partial(b.ds_lo, B, H, H));
         amax = std::max(amax, (size_t)B * H2 * H2 * b.ds.cout);
       }
       H = H2;
@@ -862,14 +884,9 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         const int t2 = pick({cur, t1});
         run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
-        if (b.has_ds && mixed_) {
-          const int lo = pick({cur, t2});
-          run_conv(b.ds_lo, buf[cur], B, H, H, buf[lo], OH, OW, Act::None, nullptr, w, s, true);
-          ident = pick({cur, t2, lo});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, buf[lo], w, s, true, true);
-        } else if (b.has_ds) {
+        if (b.has_ds) {
           ident = pick({cur, t2});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s, mixed_);
         }
         const int o = pick({cur, t2, ident});
         run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
@@ -879,14 +896,9 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         const int t1 = pick({cur});
         run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
-        if (b.has_ds && mixed_) {  // fp32 out = x . w_hi + bias + (x . w_lo)
-          const int lo = pick({cur, t1});
-          run_conv(b.ds_lo, buf[cur], B, H, H, buf[lo], OH, OW, Act::None, nullptr, w, s, true);
-          ident = pick({cur, t1, lo});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, buf[lo], w, s, true, true);
-        } else if (b.has_ds) {
+        if (b.has_ds) {  // F16M: hi + lo weights, fp32 out (the next conv's fp32 residual)
           ident = pick({cur, t1});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s);
+          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s, mixed_);
         }
         const int o = pick({cur, t1, ident});
         run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,

@@ -25,6 +25,7 @@ struct ConvW {
   int kpad = 0, npad = 0;
   size_t wplane = 0;
   Prec prec = Prec::F16;  // packing / contraction precision of this conv
+  int krep = 1;           // 2: hi + lo weight steps per A step (GemmDesc::krep; SPI_PREC_F16M)
 };
 
 struct LinearW {
@@ -33,6 +34,7 @@ struct LinearW {
   size_t wplane = 0;
   bool has_bias = true;
   Prec prec = Prec::F16;
+  int krep = 1;
 };
 
 struct LnW {
@@ -42,11 +44,7 @@ struct LnW {
 struct ResBlock {
   ConvW c1, c2, c3;  // c3 only for bottleneck
   bool has_ds = false;
-  ConvW ds;
-  // SPI_PREC_F16M: the downsample's weights as hi (ds, fp16) + lo (ds_lo, fp16 of
-  // w - hi, no bias): ds_lo runs first into an fp32 buffer that ds adds as its
-  // residual, so the conv sees the weights to ~22 bits with plain fp16 MFMAs.
-  ConvW ds_lo;
+  ConvW ds;  // SPI_PREC_F16M: packed hi + lo (krep = 2), fp32 output
 };
 
 struct TfLayer {  // BERT (post-LN) / ViT (pre-LN) encoder layer
@@ -128,7 +126,7 @@ class Model {
   int family_ = 0;
   Prec prec_ = Prec::F16;
   bool f16_ = true;  // activations stored as fp16 (Prec::F16 only)
-  bool mixed_ = false;  // SPI_PREC_F16M on a ResNet (ResBlock::ds_lo, stem / FC in F16X3)
+  bool mixed_ = false;  // SPI_PREC_F16M on a ResNet (stem in F16X3, downsample + FC with krep = 2)
   // ResNet under Prec::F16X3: conv outputs / pool inputs in the split layout
   // (GemmDesc::a_split), so the GEMM main loop never splits A on the VALU.
   bool split_ = false;

@@ -47,6 +47,11 @@ struct GemmDesc {
   // run over every pixel and average its own C tile (64 x 64 tiles, one image
   // per tile row, pool_rows <= 64).  M = images x pool_rows.
   int pool_rows = 0;
+  // krep = 2 (F16, dense or one-tap-per-step conv A): the packed W holds two k-steps per A
+  // k-step -- fp16(w) then fp16(w - fp16(w)) for the same 64 k-values -- and each A k-step is
+  // staged twice, so one launch accumulates x.w_hi + x.w_lo (~22-bit weights on fp16 MFMAs).
+  // Kpad is the packed (W) row length; K stays the logical A length.
+  int krep = 1;
 };
 
 struct GemmPtrs {
