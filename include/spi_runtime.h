@@ -122,10 +122,15 @@ typedef struct spi_job_timing {
 typedef void (*spi_job_done_fn)(void* user, int32_t request_id, int32_t status, const char* error,
                                 const spi_job_timing* timing);
 
+/* A device serves about four busy streams at once: with a fifth (four workers +
+ * a copy stream, or five workers) one or two of them get a third of the others'
+ * tasks.  SPI_H2D_AUTO keeps a device at <= 4 busy streams: a
+ * shared copy stream for <= 3 workers, the H2D on the worker stream beyond. */
 enum spi_h2d_mode {
-  SPI_H2D_DEVICE_STREAM = 0, /* one copy stream per device, event-joined (default) */
+  SPI_H2D_DEVICE_STREAM = 0, /* one copy stream per device, event-joined */
   SPI_H2D_WORKER_STREAM = 1, /* H2D on the worker's own stream */
-  SPI_H2D_WORKER_COPY = 2    /* one copy stream per worker, event-joined */
+  SPI_H2D_WORKER_COPY = 2,   /* one copy stream per worker, event-joined */
+  SPI_H2D_AUTO = 3           /* default: DEVICE_STREAM for <= 3 workers per device, else WORKER_STREAM */
 };
 
 typedef struct spi_runtime_config {
@@ -179,6 +184,11 @@ int spi_runtime_submit(spi_runtime* rt, int32_t request_id, int64_t batch, const
 int spi_runtime_drain(spi_runtime* rt);
 void spi_runtime_stats(const spi_runtime* rt, int64_t* completed, int64_t* failed);
 int32_t spi_runtime_num_workers(const spi_runtime* rt);
+/* Measurement hook: where worker `worker`'s thread spent its time so far --
+ * out[0] tasks launched, out[1] ns waiting for a free slot, out[2] ns of host
+ * staging (copy_job_inputs_to_slot), out[3] ns enqueueing H2D + codelet + D2H,
+ * out[4] ns waiting on completion events.  Returns SPI_OK or an error status. */
+int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out);
 /* Current adaptive target batch limit (samples); the fixed limit otherwise. */
 int32_t spi_runtime_batch_target(const spi_runtime* rt);
 void spi_runtime_destroy(spi_runtime* rt);

@@ -262,6 +262,9 @@ struct Worker {
   std::deque<Task> inflight;
   std::deque<Job> fixed;  // jobs pinned to this worker (under the runtime mutex)
   std::thread thread;
+  // where the worker thread's time goes (spi_runtime_worker_times): tasks, slot wait,
+  // host staging, H2D + codelet + D2H enqueue, completion-event wait (ns)
+  std::atomic<int64_t> t_tasks{0}, t_slot{0}, t_stage{0}, t_enqueue{0}, t_event{0};
 };
 
 using QueueKey = std::pair<int64_t, uint64_t>;  // (-priority, submission sequence)
@@ -363,6 +366,7 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
   SlotPool& pool = *pools[w->pool];
   Task t;
   t.jobs = std::move(jobs);
+  const int64_t c0 = now_ns();
   // a free slot: never block while this worker still holds finished work
   int s = pool.try_acquire();
   while (s < 0 && !w->inflight.empty()) {
@@ -372,6 +376,7 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
   if (s < 0) s = pool.acquire();
   t.slot = s;
   Slot& slot = pool.slots[s];
+  const int64_t c1 = now_ns();
   // copy_job_inputs_to_slot: every job's samples at its row offset
   std::vector<CopyPool::Chunk> ops;
   for (const Job& j : t.jobs) {
@@ -383,6 +388,7 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
     t.total += j.batch;
   }
   copier->copy(ops);
+  const int64_t c2 = now_ns();
   // H2D into the slot's HBM buffers (StarPU's fetch of the R handles)
   hipStream_t h2d = w->copy_stream ? w->copy_stream : w->stream;
   for (int i = 0; i < ni && t.status == SPI_OK; ++i)
@@ -456,6 +462,11 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
     ++inflight_tasks;
   }
   w->inflight.push_back(std::move(t));
+  const int64_t c3 = now_ns();
+  w->t_tasks += 1;
+  w->t_slot += c1 - c0;
+  w->t_stage += c2 - c1;
+  w->t_enqueue += c3 - c2;
 }
 
 // starpu_output_callback: wait for the task's completion event, hand each job
@@ -466,10 +477,12 @@ void spi_runtime::finalize_oldest(Worker* w) {
   w->inflight.pop_front();
   SlotPool& pool = *pools[w->pool];
   Slot& slot = pool.slots[t.slot];
+  const int64_t e0 = now_ns();
   if (hipEventSynchronize(slot.done) != hipSuccess && t.status == SPI_OK) {
     t.status = SPI_ERR_DEVICE;
     t.err = "stream synchronisation failed";
   }
+  w->t_event += now_ns() - e0;
   const int no = cfg.num_outputs;
   for (size_t k = 0; k < t.jobs.size(); ++k) {
     const Job& j = t.jobs[k];
@@ -630,7 +643,7 @@ void spi_runtime_config_init(spi_runtime_config* c) {
   c->coalesce_max_jobs = 1;
   c->pipeline_depth = 2;
   c->copy_threads = 4;
-  c->h2d_mode = SPI_H2D_DEVICE_STREAM;
+  c->h2d_mode = SPI_H2D_AUTO;
   c->batching.kind = SPI_BATCHING_FIXED;
 }
 
@@ -642,13 +655,15 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   };
   if (!c || c->num_devices < 1 || c->num_devices > SPI_MAX_REPLICAS || c->max_batch < 1 || c->num_inputs < 1 ||
       c->num_inputs > SPI_MAX_INPUTS || c->num_outputs < 1 || c->num_outputs > SPI_MAX_OUTPUTS ||
-      c->h2d_mode < 0 || c->h2d_mode > SPI_H2D_WORKER_COPY || c->batching.kind < 0 ||
+      c->h2d_mode < 0 || c->h2d_mode > SPI_H2D_AUTO || c->batching.kind < 0 ||
       c->batching.kind > SPI_BATCHING_ADAPTIVE)
     return fail("invalid runtime configuration");
   auto rt = std::make_unique<spi_runtime>();
   rt->cfg = *c;
   spi_runtime_config& cfg = rt->cfg;
   if (cfg.workers_per_device <= 0) cfg.workers_per_device = 4;
+  if (cfg.h2d_mode == SPI_H2D_AUTO)
+    cfg.h2d_mode = cfg.workers_per_device <= 3 ? SPI_H2D_DEVICE_STREAM : SPI_H2D_WORKER_STREAM;
   if (cfg.pipeline_depth <= 0) cfg.pipeline_depth = 2;
   if (cfg.copy_threads <= 0) cfg.copy_threads = 4;
   if (cfg.slots_per_device <= 0) cfg.slots_per_device = std::max(2, cfg.workers_per_device * cfg.pipeline_depth);
@@ -809,6 +824,17 @@ void spi_runtime_stats(const spi_runtime* rt, int64_t* completed, int64_t* faile
 }
 
 int32_t spi_runtime_num_workers(const spi_runtime* rt) { return rt ? (int32_t)rt->workers.size() : 0; }
+
+int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out) {
+  if (!rt || !out || worker < 0 || worker >= (int32_t)rt->workers.size()) return SPI_ERR_INVALID_ARGUMENT;
+  const auto& w = *rt->workers[worker];
+  out[0] = w.t_tasks.load();
+  out[1] = w.t_slot.load();
+  out[2] = w.t_stage.load();
+  out[3] = w.t_enqueue.load();
+  out[4] = w.t_event.load();
+  return SPI_OK;
+}
 
 int32_t spi_runtime_batch_target(const spi_runtime* rt) {
   if (!rt) return 0;

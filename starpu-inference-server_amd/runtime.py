@@ -17,7 +17,7 @@ from .codelet import ModelReplica, spi_dtype
 
 SPI_ERR_QUEUE_FULL = 8
 BATCHING = {"fixed": 0, "disabled": 1, "adaptive": 2}
-H2D_MODES = {"device_stream": 0, "worker_stream": 1, "worker_copy": 2}
+H2D_MODES = {"device_stream": 0, "worker_stream": 1, "worker_copy": 2, "auto": 3}
 
 
 class JobTiming(C.Structure):
@@ -109,6 +109,7 @@ for _name, _res, _args in [
     ("spi_runtime_drain", C.c_int, [C.c_void_p]),
     ("spi_runtime_stats", None, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("spi_runtime_num_workers", C.c_int32, [C.c_void_p]),
+    ("spi_runtime_worker_times", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
     ("spi_runtime_batch_target", C.c_int32, [C.c_void_p]),
     ("spi_runtime_destroy", None, [C.c_void_p]),
     ("spi_runtime_loadgen", C.c_int, [C.c_void_p, C.POINTER(LoadgenConfig), C.POINTER(C.c_void_p),
@@ -168,7 +169,7 @@ class Runtime:
     def __init__(self, replicas: list[ModelReplica], input_specs, output_specs, max_batch: int,
                  workers_per_device: int = 4, max_queue: int = 0, coalesce_max_jobs: int = 1,
                  coalesce_delay_us: int = 0, pipeline_depth: int = 2, slots_per_device: int = 0,
-                 copy_threads: int = 4, h2d_mode: str = "device_stream", min_priority: int = 0,
+                 copy_threads: int = 4, h2d_mode: str = "auto", min_priority: int = 0,
                  max_priority: int = 0, batching: BatchingConfig | None = None):
         """input_specs: [(per-sample shape, dtype)]; output_specs: [(per-sample elems, dtype)].
         Fixed batching (default): coalesce_max_jobs > 1 merges up to that many queued jobs (while
@@ -218,6 +219,18 @@ class Runtime:
     @property
     def num_workers(self) -> int:
         return lib.spi_runtime_num_workers(self.handle)
+
+    def worker_times(self) -> list[dict]:
+        """Per worker: tasks launched and the seconds its thread spent waiting for slots, staging
+        inputs, enqueueing H2D + codelet + D2H and waiting on completion events."""
+        out = []
+        for w in range(self.num_workers):
+            v = (C.c_int64 * 5)()
+            if lib.spi_runtime_worker_times(self.handle, w, v) != N.SPI_OK:
+                raise RuntimeError("spi_runtime_worker_times failed")
+            out.append(dict(tasks=v[0], slot_s=v[1] / 1e9, stage_s=v[2] / 1e9, enqueue_s=v[3] / 1e9,
+                            event_s=v[4] / 1e9))
+        return out
 
     @property
     def batch_target(self) -> int:

@@ -2,6 +2,8 @@
 slots -> H2D -> HIP codelet -> D2H -> caller buffers, checked against the oracle."""
 import importlib
 
+import time
+
 import numpy as np
 import pytest
 
@@ -208,7 +210,8 @@ def test_runtime_fixed_worker_and_priority(spi, zoo, rtmod):
     yb = [np.zeros((8, 1000), np.float32) for _ in range(2)]
     xs = np.random.default_rng(11).random((1, 3, 224, 224), dtype=np.float32)
     small = [np.zeros((1, 1000), np.float32) for _ in range(6)]
-    rt.submit(100, [xb], [yb[0]])          # occupies the only worker
+    rt.submit(100, [xb], [yb[0]])          # occupies the only worker (fp32 ResNet-152 bs8: several ms)
+    time.sleep(0.001)                      # let the worker dequeue it before the rest arrive
     rt.submit(101, [xb], [yb[1]])          # queued behind it, so the next three queue too
     for k, rid in enumerate([5, 3, 4]):     # default priorities 95, 97, 96
         rt.submit(rid, [xs], [small[k]])
