@@ -124,6 +124,15 @@ struct KArgs {
   // padding around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel
   // blocks, h_bps of them per split-K slice
   int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
+  int splits;  // split-K slices (the grid holds tiles x splits workgroups of this problem)
+};
+
+// One launch, one or two independent problems of the same kernel instance (a
+// grouped launch: ResNet's downsample 1x1 conv beside its block's first conv,
+// both reading the block input).  Workgroups [0, wgs0) run a[0], the rest a[1].
+struct KGroup {
+  KArgs a[2];
+  int wgs0;
 };
 
 template <int MODE>
@@ -253,8 +262,11 @@ constexpr int kMinWaves = std::max(
 
 // NW waves per workgroup in an (NW / 2) x 2 grid over the tile: wave (wm, wn)
 // owns rows [wm * BM / (NW / 2), ...) x columns [wn * BN / 2, ...).
-template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
-__global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel(KArgs a) {
+// The workgroup body: problem `a`, split-K slice `kslice`, linear tile `lin`.
+// gemm_kernel passes its own arguments (constant kernarg offsets, preloadable);
+// gemm_kernel_pair selects one of two problems at run time.
+template <int MODE, int BM, int BN, int STAGES, int KIND, int NW>
+__device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, const int lin) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
@@ -282,7 +294,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
-  int tile = blockIdx.x;
+  int tile = lin;
   {
     const int nwg = a.tiles, q = nwg >> 3, r = nwg & 7, x = tile & 7, l = tile >> 3;
     if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
@@ -335,10 +347,10 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
     return (ty < a.h_th && img < d.M / (d.OH * d.OW) && (unsigned)oy < (unsigned)d.OH) ? (img * d.OH + oy) * d.OW + tx
                                                                                       : -1;
   };
-  const int kbeg = blockIdx.y * a.k_per_split;
+  const int kbeg = kslice * a.k_per_split;
   const int kend = min(d.Kpad, kbeg + a.k_per_split);
   // halo: channel blocks [h_b0, h_b1) of this split-K slice, 9 taps each
-  const int h_b0 = HALO ? blockIdx.y * a.h_bps : 0;
+  const int h_b0 = HALO ? kslice * a.h_bps : 0;
   const int h_b1 = HALO ? min(a.h_nblk, h_b0 + a.h_bps) : 0;
   const int nsteps = HALO ? (h_b1 - h_b0) * 9 : (kend - kbeg) / ESTEP;
 
@@ -1001,15 +1013,15 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   SPI_STAMP(st_d);
 #ifdef SPI_GEMM_STAMPS
   if (tid == 0) {
-    unsigned long long* g = g_gemm_stamps + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) & 65535) * 8;
-    g[0] = st_d - st_t0;
-    g[1] = st_wait;
-    g[2] = st_issue;
-    g[3] = st_comp;
-    g[4] = (unsigned long long)nsteps;
+    unsigned long long* gs = g_gemm_stamps + (size_t)(blockIdx.x & 65535) * 8;
+    gs[0] = st_d - st_t0;
+    gs[1] = st_wait;
+    gs[2] = st_issue;
+    gs[3] = st_comp;
+    gs[4] = (unsigned long long)nsteps;
   }
 #endif
-  if (!kSplitK<BM, BN, KIND> || gridDim.y == 1) {
+  if (!kSplitK<BM, BN, KIND> || a.splits == 1) {
     finish(acc);
     return;
   }
@@ -1020,7 +1032,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   // contiguous bytes at ((i*TJ + j)*NT + tid)*16), write-through (sc1) so no
   // release fence is needed; the ticket is a relaxed agent-scope atomic; the
   // reducer reads every slab with sc1 loads.  Same thread <-> (m, n) map as above.
-  const int splits = gridDim.y;
+  const int splits = a.splits;
   constexpr int SLAB = BM * BN;
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
@@ -1029,7 +1041,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const int off = (blockIdx.y * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+      const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
     }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1073,6 +1085,22 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   }
 }
 
+template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel(KArgs a) {
+  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, blockIdx.y, blockIdx.x);
+}
+
+// Grouped launch (KGroup): 1-D grid, problem-major, then slice, then tile.
+template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel_pair(KGroup g) {
+  int lin = blockIdx.x;
+  const bool second = lin >= g.wgs0;
+  if (second) lin -= g.wgs0;
+  const KArgs& a = second ? g.a[1] : g.a[0];
+  const int kslice = lin / a.tiles;
+  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, kslice, lin - kslice * a.tiles);
+}
+
 struct Plan {
   int bm, bn, stages, splits, k_per_split;
   // kConvHalo: waves per workgroup, virtual output rows per band, the virtual-row
@@ -1101,6 +1129,7 @@ struct Knobs {
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
   int halo_stages = 3, halo_minh = 14;
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
+  int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
   struct HaloPick {
@@ -1134,6 +1163,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
     // (OW 0 = any other width; rows 0 = not a halo conv)
@@ -1335,13 +1365,14 @@ void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
   }
 }
 
+// Kernel arguments of one problem under its plan.
 template <int MODE>
-void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
-  const Plan pl = choose_plan(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE);
+KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   KArgs a{};
   a.d = d;
   a.p = p;
   a.k_per_split = pl.k_per_split;
+  a.splits = pl.splits;
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
   xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, a.tiles_m, a.tiles / a.tiles_m, a.xg_m, a.xg_n);
@@ -1351,47 +1382,107 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP && d.KH * d.KW <= 31;
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   a.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res)));
-  const dim3 grid(a.tiles, pl.splits);
+  if (pl.halo) {
+    a.h_th = pl.th;
+    a.h_period = pl.period;
+    a.h_off = pl.off;
+    a.h_hwp = d.W + 2 * d.pad;
+    a.h_hp = (pl.th + 2) * a.h_hwp;
+    a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
+    a.h_bps = pl.bps;
+  }
+  return a;
+}
+
+// One problem under its plan: grid tiles x splits.
+template <int MODE>
+void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
+  const dim3 grid(g.tiles, pl.splits);
   if (pl.halo) {
     if constexpr (MODE != (int)Prec::F16X3) {  // fp32 A is split at fragment read: not a halo mode
-      a.h_th = pl.th;
-      a.h_period = pl.period;
-      a.h_off = pl.off;
-      a.h_hwp = d.W + 2 * d.pad;
-      a.h_hp = (pl.th + 2) * a.h_hwp;
-      a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
-      a.h_bps = pl.bps;
       if (pl.bm == 256 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 4, kConvHalo, 8>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 4, kConvHalo, 8>), grid, dim3(512), 0, s, g);
       else if (pl.bm == 256)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, g);
       else if (pl.bm == 128 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 4, kConvHalo>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 4, kConvHalo>), grid, dim3(256), 0, s, g);
       else if (pl.bm == 128)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
       else if (pl.halo == 2 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHaloS>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHaloS>), grid, dim3(256), 0, s, g);
       else if (pl.halo == 2)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, g);
       else if (pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHalo>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHalo>), grid, dim3(256), 0, s, g);
       else
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
     }
     return;
   }
   if (pl.bm == 128 && pl.bn == 128)
-    launch_tile<MODE, 128, 128, 2>(a, grid, s);
+    launch_tile<MODE, 128, 128, 2>(g, grid, s);
   else if (pl.bm == 128 && pl.stages == 2)
-    launch_tile<MODE, 128, 64, 2>(a, grid, s);
+    launch_tile<MODE, 128, 64, 2>(g, grid, s);
   else if (pl.bm == 128)
-    launch_tile<MODE, 128, 64, 3>(a, grid, s);
+    launch_tile<MODE, 128, 64, 3>(g, grid, s);
   else if (pl.stages == 2)
-    launch_tile<MODE, 64, 64, 2>(a, grid, s);
+    launch_tile<MODE, 64, 64, 2>(g, grid, s);
   else if (pl.stages == 4)
-    launch_tile<MODE, 64, 64, 4>(a, grid, s);
+    launch_tile<MODE, 64, 64, 4>(g, grid, s);
   else
-    launch_tile<MODE, 64, 64, 3>(a, grid, s);
+    launch_tile<MODE, 64, 64, 3>(g, grid, s);
+}
+
+// Two tap-walk conv problems sharing pl's tile shape and ring depth: one launch.
+template <int MODE>
+void dispatch_pair(const Plan& pl, const KGroup& g, int wgs, hipStream_t s) {
+  const dim3 grid(wgs);
+  if (pl.bm == 128 && pl.bn == 128)
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 128, 2, kConvTap>), grid, dim3(256), 0, s, g);
+  else if (pl.bm == 128 && pl.stages == 2)
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
+  else if (pl.bm == 128)
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
+  else if (pl.stages == 2)
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
+  else if (pl.stages == 4)
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 4, kConvTap>), grid, dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
+}
+
+constexpr Prec prec_of_mode(int mode) { return mode == kF16X3S ? Prec::F16X3 : (Prec)mode; }
+
+template <int MODE>
+void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
+  const Plan pl = choose_plan(d, prec_of_mode(MODE));
+  dispatch<MODE>(pl, make_args<MODE>(d, p, pl), s);
+}
+
+// Two problems in one launch when their plans share a kernel instance (same
+// tile, ring depth and A kind, neither a halo plan); otherwise two launches.
+// Problem 1's split-K slabs and tickets follow problem 0's in the workspace.
+template <int MODE>
+void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, hipStream_t s) {
+  const Prec pr = prec_of_mode(MODE);
+  const Plan q0 = choose_plan(d0, pr), q1 = choose_plan(d1, pr);
+  KGroup g{};
+  g.a[0] = make_args<MODE>(d0, p0, q0);
+  GemmPtrs p1s = p1;
+  if (q0.splits > 1) {  // keep clear of problem 0's slabs / tickets
+    p1s.partial = p0.partial + (size_t)g.a[0].tiles * q0.splits * q0.bm * q0.bn;
+    p1s.counters = p0.counters + g.a[0].tiles;
+  }
+  g.a[1] = make_args<MODE>(d1, p1s, q1);
+  const bool same = knobs().pair && !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
+                    q0.stages == q1.stages && g.a[0].cell_uniform && g.a[1].cell_uniform;
+  if (!same) {
+    launch<MODE>(d0, p0, s);
+    launch<MODE>(d1, p1, s);
+    return;
+  }
+  g.wgs0 = g.a[0].tiles * q0.splits;
+  dispatch_pair<MODE>(q0, g, g.wgs0 + g.a[1].tiles * q1.splits, s);
 }
 
 }  // namespace
@@ -1418,12 +1509,45 @@ extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
 }
 #endif
 
-void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
+namespace {
+void check_desc(const GemmDesc& d, Prec prec) {
   if (d.pool_rows && (d.conv || d.pool_rows > 64 || d.M % d.pool_rows))
     throw std::invalid_argument("pooled GEMM: dense A, pool_rows <= 64 dividing M");
   if (d.krep != 1 && (d.krep != 2 || prec != Prec::F16 || d.Kpad % (2 * estep_of(prec)) ||
                       (d.conv && (d.Cin < estep_of(prec) || d.KH * d.KW > 31))))
     throw std::invalid_argument("krep = 2 needs F16, a packed Kpad of whole step pairs and dense or one-tap-per-step A");
+  if (prec == Prec::F16X3 && d.a_split && d.conv && (d.Cin < 32 || d.KH * d.KW > 31))
+    throw std::invalid_argument("split activations need Cin >= 32 and <= 31 filter taps");
+}
+}  // namespace
+
+void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, Prec prec,
+               hipStream_t s) {
+  check_desc(d0, prec);
+  check_desc(d1, prec);
+  if (prec == Prec::F16X3 && d0.a_split != d1.a_split) {
+    gemm(d0, p0, prec, s);
+    gemm(d1, p1, prec, s);
+    return;
+  }
+  switch (prec) {
+    case Prec::F16:
+      launch_pair<(int)Prec::F16>(d0, p0, d1, p1, s);
+      break;
+    case Prec::F32:
+      launch_pair<(int)Prec::F32>(d0, p0, d1, p1, s);
+      break;
+    case Prec::F16X3:
+      if (d0.a_split)
+        launch_pair<kF16X3S>(d0, p0, d1, p1, s);
+      else
+        launch_pair<(int)Prec::F16X3>(d0, p0, d1, p1, s);
+      break;
+  }
+}
+
+void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
+  check_desc(d, prec);
   switch (prec) {
     case Prec::F16:
       launch<(int)Prec::F16>(d, p, s);
@@ -1433,8 +1557,6 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
       break;
     case Prec::F16X3:
       // split A relies on one (kh, kw) cell per 32-k step (byte-identical to fp32 addressing)
-      if (d.a_split && d.conv && (d.Cin < 32 || d.KH * d.KW > 31))
-        throw std::invalid_argument("split activations need Cin >= 32 and <= 31 filter taps");
       if (d.a_split)
         launch<kF16X3S>(d, p, s);
       else

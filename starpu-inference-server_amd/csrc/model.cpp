@@ -648,9 +648,11 @@ size_t Model::linear_partial(const LinearW& L, int M) const {
   return gemm_partial_floats(linear_desc(L, M, L.k, L.n), L.prec);
 }
 
-void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
-                     Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32, bool res_f32) {
-  GemmDesc d = conv_desc(c, B, H, W, OH, OW);
+Model::ConvCall Model::conv_call(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
+                                 Act act, const void* res, Workspace& ws, bool out_f32, bool res_f32) const {
+  ConvCall k;
+  GemmDesc& d = k.d;
+  d = conv_desc(c, B, H, W, OH, OW);
   d.act = act;
   d.wplane = c.wplane;
   d.out_split = split_;
@@ -659,11 +661,11 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   d.res_f32 = res_f32;
   d.out_f16 = f16_ && c.prec == Prec::F16X3 && !out_f32;  // F16M stem: F16X3 contraction, fp16 activations
   const size_t es = f16_ ? 2 : 4;
-  const int nrep = !prof_ ? 1 : op_begin(s, "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
-                    std::to_string(c.cout) + "_s" + std::to_string(c.stride) + "_M" + std::to_string(d.M),
-             2.0 * d.M * d.N * (double)c.kh * c.kw * c.cin,
-             (double)B * H * W * c.cin_pad * es + (double)c.cout * d.K * es + (double)d.M * d.N * es * (res ? 2 : 1));
-  GemmPtrs p;
+  k.name = "conv" + std::to_string(c.kh) + "x" + std::to_string(c.kw) + "_c" + std::to_string(c.cin) + "_k" +
+           std::to_string(c.cout) + "_s" + std::to_string(c.stride) + "_M" + std::to_string(d.M);
+  k.flops = 2.0 * d.M * d.N * (double)c.kh * c.kw * c.cin;
+  k.bytes = (double)B * H * W * c.cin_pad * es + (double)c.cout * d.K * es + (double)d.M * d.N * es * (res ? 2 : 1);
+  GemmPtrs& p = k.p;
   p.A = x;
   p.W = ptr<void>(c.w);
   p.bias = ptr<float>(c.b);
@@ -672,9 +674,37 @@ void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
-  if (gemm_partial_floats(d, c.prec) > ws.partial_floats || gemm_counter_slots(d, c.prec) > kCounterSlots)
+  k.prec = c.prec;
+  return k;
+}
+
+void Model::run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
+                     Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32, bool res_f32) {
+  const ConvCall k = conv_call(c, x, B, H, W, y, OH, OW, act, res, ws, out_f32, res_f32);
+  if (gemm_partial_floats(k.d, k.prec) > ws.partial_floats || gemm_counter_slots(k.d, k.prec) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
-  for (int r = 0; r < nrep; ++r) gemm(d, p, c.prec, s);
+  const int nrep = !prof_ ? 1 : op_begin(s, k.name, k.flops, k.bytes);
+  for (int r = 0; r < nrep; ++r) gemm(k.d, k.p, k.prec, s);
+  if (prof_) op_end(s);
+}
+
+// A block's first conv and its downsample conv read the same input: one grouped
+// launch (gemm_pair) instead of two dependent ones.
+void Model::run_conv_pair(const ConvW& c0, const void* x, int B, int H, int W, void* y0, int& OH0, int& OW0,
+                          Act act0, const ConvW& c1, void* y1, bool out1_f32, Workspace& ws, hipStream_t s) {
+  int OH1, OW1;
+  const ConvCall k0 = conv_call(c0, x, B, H, W, y0, OH0, OW0, act0, nullptr, ws, false, false);
+  const ConvCall k1 = conv_call(c1, x, B, H, W, y1, OH1, OW1, Act::None, nullptr, ws, out1_f32, false);
+  if (k0.prec != k1.prec) {
+    run_conv(c0, x, B, H, W, y0, OH0, OW0, act0, nullptr, ws, s);
+    run_conv(c1, x, B, H, W, y1, OH1, OW1, Act::None, nullptr, ws, s, out1_f32);
+    return;
+  }
+  if (gemm_partial_floats(k0.d, k0.prec) + gemm_partial_floats(k1.d, k1.prec) > ws.partial_floats ||
+      gemm_counter_slots(k0.d, k0.prec) + gemm_counter_slots(k1.d, k1.prec) > kCounterSlots)
+    throw std::runtime_error("split-K workspace too small");
+  const int nrep = !prof_ ? 1 : op_begin(s, k0.name + "+" + k1.name, k0.flops + k1.flops, k0.bytes + k1.bytes);
+  for (int r = 0; r < nrep; ++r) gemm_pair(k0.d, k0.p, k1.d, k1.p, k0.prec, s);
   if (prof_) op_end(s);
 }
 
@@ -761,6 +791,8 @@ Workspace* Model::workspace(hipStream_t s) {
     H = (H + 2 - 3) / 2 + 1;
     for (const auto& b : blocks_) {
       int H2;
+      if (b.has_ds)  // conv1 + downsample in one grouped launch (run_conv_pair)
+        partial = std::max(partial, conv_partial(b.c1, B, H, H) + conv_partial(b.ds, B, H, H));
       if (bottleneck_) {
         partial = std::max(partial, conv_partial(b.c1, B, H, H));
         amax = std::max(amax, (size_t)B * H * H * b.c1.cout);
@@ -880,25 +912,27 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       int H2;
       if (bottleneck_) {
         const int t1 = pick({cur});
-        run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w, s);
-        const int t2 = pick({cur, t1});
-        run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
-        if (b.has_ds) {
-          ident = pick({cur, t2});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s, mixed_);
+        if (b.has_ds) {  // the downsample reads the block input too: grouped with conv1
+          ident = pick({cur, t1});
+          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, b.ds, buf[ident], mixed_, w, s);
+        } else {
+          run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w, s);
         }
+        const int t2 = pick({cur, t1, ident});
+        run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         const int o = pick({cur, t2, ident});
         run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
                  mixed_ && b.has_ds);
         cur = o;
       } else {
         const int t1 = pick({cur});
-        run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         int ident = cur;
         if (b.has_ds) {  // F16M: hi + lo weights, fp32 out (the next conv's fp32 residual)
           ident = pick({cur, t1});
-          run_conv(b.ds, buf[cur], B, H, H, buf[ident], OH, OW, Act::None, nullptr, w, s, mixed_);
+          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, b.ds, buf[ident], mixed_, w, s);
+        } else {
+          run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         }
         const int o = pick({cur, t1, ident});
         run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,

@@ -113,6 +113,17 @@ class Model {
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
                 Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32 = false,
                 bool res_f32 = false);
+  struct ConvCall {
+    GemmDesc d;
+    GemmPtrs p;
+    Prec prec = Prec::F16;
+    std::string name;
+    double flops = 0, bytes = 0;
+  };
+  ConvCall conv_call(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW, Act act,
+                     const void* res, Workspace& ws, bool out_f32, bool res_f32) const;
+  void run_conv_pair(const ConvW& c0, const void* x, int B, int H, int W, void* y0, int& OH0, int& OW0, Act act0,
+                     const ConvW& c1, void* y1, bool out1_f32, Workspace& ws, hipStream_t s);
   bool pooled_fc(int hw) const;
   void run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s);
   size_t conv_partial(const ConvW& c, int B, int H, int W) const;

@@ -71,6 +71,12 @@ size_t gemm_counter_slots(const GemmDesc& d, Prec prec);
 // k-values per staged step (W rows must be padded to a multiple of it).
 int gemm_kstep(Prec prec);
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s);
+// Two independent problems of one precision in a single launch when their plans
+// share a kernel instance (else two launches); problem 1's split-K slabs and
+// tickets follow problem 0's (size the workspace for both: gemm_partial_floats /
+// gemm_counter_slots summed).
+void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, Prec prec,
+               hipStream_t s);
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
