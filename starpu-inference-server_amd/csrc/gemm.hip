@@ -271,7 +271,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, cons
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
   constexpr int NT = 64 * NW;  // threads per workgroup
-  static_assert(NW == 4 || (NW == 8 && HALO), "8-wave workgroups: halo kinds only");
+  static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
@@ -1130,6 +1130,7 @@ struct Knobs {
   int halo_stages = 3, halo_minh = 14;
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
   int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
+  int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
   struct HaloPick {
@@ -1164,6 +1165,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_BIG"); e && *e) k.big = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
     // (OW 0 = any other width; rows 0 = not a halo conv)
@@ -1328,6 +1330,14 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
     const int T = k.target;
+    // 256x128 tiles, 8 waves (2 per SIMD), 3 stages: a quarter fewer staging
+    // instructions per MFMA than 128x128 (SPI_GEMM_BIG=1; off by default: ViT-L -4 %, 4096^3 -3 %)
+    if (k.big && d.N > 64 && !d.pool_rows && tiles_of(256, 128) >= T) {
+      Plan p = finish_plan(Plan{256, 128, 3, 1, 0}, ksteps, ES, d.krep);
+      p.nw = 8;
+      p.stages = 3;
+      return p;
+    }
     if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
     if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
     const int t64 = tiles_of(64, 64);
@@ -1353,15 +1363,15 @@ int ilog2(int v) {
   return s;
 }
 
-template <int MODE, int BM, int BN, int STAGES>
+template <int MODE, int BM, int BN, int STAGES, int NW = 4>
 void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
   if (a.cell_uniform) {
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvTap>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvTap, NW>), grid, dim3(64 * NW), 0, s, a);
   } else if (a.d.conv) {
     if constexpr (MODE != kF16X3S)  // split A needs one tap per step (checked in gemm())
-      hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvGen>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvGen, NW>), grid, dim3(64 * NW), 0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kDense>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kDense, NW>), grid, dim3(64 * NW), 0, s, a);
   }
 }
 
@@ -1419,7 +1429,9 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
     }
     return;
   }
-  if (pl.bm == 128 && pl.bn == 128)
+  if (pl.bm == 256)
+    launch_tile<MODE, 256, 128, 3, 8>(g, grid, s);
+  else if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(g, grid, s);
   else if (pl.bm == 128 && pl.stages == 2)
     launch_tile<MODE, 128, 64, 2>(g, grid, s);
@@ -1475,7 +1487,8 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
   }
   g.a[1] = make_args<MODE>(d1, p1s, q1);
   const bool same = knobs().pair && !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
-                    q0.stages == q1.stages && g.a[0].cell_uniform && g.a[1].cell_uniform;
+                    q0.stages == q1.stages && q0.nw == 4 && q1.nw == 4 && g.a[0].cell_uniform &&
+                    g.a[1].cell_uniform;
   if (!same) {
     launch<MODE>(d0, p0, s);
     launch<MODE>(d1, p1, s);

@@ -36,7 +36,7 @@ def test_gemm_identity_asymmetric(ops):
 
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("M,N,K", [(1, 1000, 512), (8, 1000, 2048), (100, 72, 96), (1024, 768, 3072),
-                                   (392, 512, 4608), (3152, 3072, 1024)])
+                                   (392, 512, 4608), (3152, 3072, 1024), (6144, 1000, 256)])
 @pytest.mark.parametrize("act", [None, "relu", "gelu"])
 def test_gemm_bias_residual_act(ops, prec, M, N, K, act):
     g = torch.Generator().manual_seed(M * 7 + N + K)
@@ -158,7 +158,8 @@ def test_conv2d_split_layout(ops, B, H, cin, cout, k, stride, res):
     assert err < 1e-5, f"split conv {B}x{H}x{cin}->{cout} k{k}s{stride}: {err:.3e}"
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (100, 96, 160), (392, 512, 4608), (1024, 768, 3072)])
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (100, 96, 160), (392, 512, 4608), (1024, 768, 3072),
+                                   (3152, 3072, 1024)])
 def test_gemm_split_layout(ops, M, N, K):
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
@@ -252,3 +253,37 @@ def test_conv_halo_candidates_fp16(ops, halo_cfg, cfg, B, H, cin, cout):
     out = ops.conv2d("fp16", x_in.cuda(), wp, cout, 3, 3, 1, 1, act="relu")
     err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
     assert err < 2e-3, f"fp16 halo {cfg} conv {B}x{H}x{cin}->{cout}: {err:.3e}"
+
+
+@pytest.fixture
+def big_tiles(ops):
+    import os
+    os.environ["SPI_GEMM_BIG"] = "1"
+    ops.lib.spi_debug_gemm_reload_env()
+    yield
+    os.environ.pop("SPI_GEMM_BIG", None)
+    ops.lib.spi_debug_gemm_reload_env()
+
+
+@pytest.mark.parametrize("prec", PRECS + ["fp16x3s"])
+@pytest.mark.parametrize("M,N,K", [(3152, 3072, 1024), (6144, 1000, 256)])
+def test_gemm_256x128_eight_waves(ops, big_tiles, prec, M, N, K):
+    """The opt-in 256x128 / 8-wave tiles (SPI_GEMM_BIG=1) on grids large enough to take them."""
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    if prec == "fp16x3s":
+        As = ops.to_split(A)
+        ref = ops.from_split(As) @ W.T + b
+        out = ops.gemm(prec, As.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda())
+        got = ops.from_split(out.cpu()) if out.dtype != torch.float32 or out.shape[1] != N else out.cpu()
+        err = normalized_max_error(got.numpy(), ref.numpy())
+        assert err < 1e-5
+        return
+    dt = ops.act_dtype(prec)
+    A_in = A.to(dt)
+    ref = A_in.float() @ (W.half().float() if prec == "fp16" else W).T + b
+    out = ops.gemm(prec, A_in.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda())
+    err = normalized_max_error(out.cpu().numpy(), ref.numpy())
+    assert err < TOL[prec], f"{prec} {M}x{N}x{K}: {err:.3e}"
