@@ -59,6 +59,17 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
 int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, int32_t C, const void* W_packed,
                       int32_t N, const float* bias, float* y, int32_t act, void* workspace, void* stream);
 
+/* Fused ResNet stem: x NCHW fp32 [B][3][H][W] -> 7x7/s2/p3 conv (64 channels,
+ * BN folded into w / bias) + ReLU -> 3x3/s2/p1 max pool -> y NHWC [B][PH][PW][64].
+ * precision 1: fp16 operands, fp16 y; 2: hi + lo fp16 operands (fp32-grade), fp16 y
+ * (the fp16m stem); 3: as 2 with y in the split layout.  W_packed: spi_op_stem_pool_bytes()
+ * of device memory filled from spi_op_stem_pool_pack(w_host fp32 [64][3][7][7]).
+ * rows_per_block: pooled rows per workgroup (0 = default 1, or 2).  W <= 224. */
+size_t spi_op_stem_pool_bytes(void);
+int spi_op_stem_pool_pack(const float* w_host, void* dst_host);
+int spi_op_stem_pool(int32_t precision, const float* x, int32_t B, int32_t H, int32_t W,
+                     const void* W_packed, const float* bias, void* y, int32_t rows_per_block, void* stream);
+
 /* Multi-head attention over packed qkv [B*S][3*D] (fp16 or fp32), head_dim 64. */
 int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias, void* ctx,
                      int32_t B, int32_t S, int32_t heads, float scale, void* stream);

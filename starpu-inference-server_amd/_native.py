@@ -210,6 +210,10 @@ _PROTOS = {
                                 C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "spi_op_avgpool_fc": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                     C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "spi_op_stem_pool_bytes": (C.c_size_t, []),
+    "spi_op_stem_pool_pack": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "spi_op_stem_pool": (C.c_int, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_int32, C.c_void_p]),
     "spi_op_attention": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                    C.c_float, C.c_void_p]),
     "spi_op_layernorm": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

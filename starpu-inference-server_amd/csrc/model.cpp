@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
@@ -119,15 +120,60 @@ size_t pack_vec(const float* v, int n) { return g_blob->add(v, (size_t)n * sizeo
 // (kh*KW + kw)*cin_pad + c; bias' = beta - mean * gamma / sqrt(var + eps).
 // hilo (F16 only): pack every 64-k block of the folded weights twice -- fp16(w), then
 // fp16(w - fp16(w)) -- for a krep = 2 contraction (GemmDesc::krep).
-ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
-                int cin_pad, Prec prec, float bn_eps, bool hilo = false) {
+// Eval BatchNorm folded into a conv: w' = w * gamma / sqrt(var + eps) (fp64, then
+// fp32), bias' = beta - mean * gamma / sqrt(var + eps) (or the conv's own bias).
+struct FoldedConv {
+  int cout = 0, cin = 0, kh = 1, kw = 1;
+  std::vector<float> w;  // [cout][cin][kh][kw]
+  std::vector<float> b;  // [cout]
+};
+
+FoldedConv fold_conv(const PMap& p, const std::string& wname, const std::string& bn, float bn_eps) {
   const spi_named_tensor* wt = need(p, wname + ".weight");
   if (wt->ndim != 4) throw std::runtime_error(wname + ".weight must be 4-D");
+  FoldedConv f;
+  f.cout = (int)wt->shape[0];
+  f.cin = (int)wt->shape[1];
+  f.kh = (int)wt->shape[2];
+  f.kw = (int)wt->shape[3];
+  std::vector<double> scale(f.cout, 1.0), shift(f.cout, 0.0);
+  if (!bn.empty()) {
+    const float* g = fdata(need(p, bn + ".weight"));
+    const float* b = fdata(need(p, bn + ".bias"));
+    const float* m = fdata(need(p, bn + ".running_mean"));
+    const float* v = fdata(need(p, bn + ".running_var"));
+    for (int o = 0; o < f.cout; ++o) {
+      const double s = (double)g[o] / std::sqrt((double)v[o] + (double)bn_eps);
+      scale[o] = s;
+      shift[o] = (double)b[o] - (double)m[o] * s;
+    }
+  } else if (has(p, wname + ".bias")) {
+    const float* b = fdata(need(p, wname + ".bias"));
+    for (int o = 0; o < f.cout; ++o) shift[o] = b[o];
+  }
+  const float* w = fdata(wt);
+  const size_t per = (size_t)f.cin * f.kh * f.kw;
+  f.w.resize((size_t)f.cout * per);
+  f.b.resize(f.cout);
+  for (int o = 0; o < f.cout; ++o) {
+    for (size_t i = 0; i < per; ++i) f.w[o * per + i] = (float)((double)w[o * per + i] * scale[o]);
+    f.b[o] = (float)shift[o];
+  }
+  return f;
+}
+
+// Conv weight [Cout][Cin][KH][KW] (+ eval BN) -> folded [Npad][Kpad], k =
+// (kh*KW + kw)*cin_pad + c.
+// hilo (F16 only): pack every 64-k block of the folded weights twice -- fp16(w), then
+// fp16(w - fp16(w)) -- for a krep = 2 contraction (GemmDesc::krep).
+ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, int stride,
+                int cin_pad, Prec prec, float bn_eps, bool hilo = false) {
+  const FoldedConv f = fold_conv(p, wname, bn, bn_eps);
   ConvW c;
-  c.cout = (int)wt->shape[0];
-  c.cin = (int)wt->shape[1];
-  c.kh = (int)wt->shape[2];
-  c.kw = (int)wt->shape[3];
+  c.cout = f.cout;
+  c.cin = f.cin;
+  c.kh = f.kh;
+  c.kw = f.kw;
   c.stride = stride;
   c.pad = c.kh / 2;
   c.cin_pad = std::max(cin_pad, c.cin);
@@ -135,29 +181,13 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
   c.kpad = round_up(K, 64);
   c.npad = round_up(c.cout, 128);
   if (hilo && prec != Prec::F16) throw std::runtime_error("hi/lo weight packing is an F16 layout");
-  std::vector<double> scale(c.cout, 1.0), shift(c.cout, 0.0);
-  if (!bn.empty()) {
-    const float* g = fdata(need(p, bn + ".weight"));
-    const float* b = fdata(need(p, bn + ".bias"));
-    const float* m = fdata(need(p, bn + ".running_mean"));
-    const float* v = fdata(need(p, bn + ".running_var"));
-    for (int o = 0; o < c.cout; ++o) {
-      const double s = (double)g[o] / std::sqrt((double)v[o] + (double)bn_eps);
-      scale[o] = s;
-      shift[o] = (double)b[o] - (double)m[o] * s;
-    }
-  } else if (has(p, wname + ".bias")) {
-    const float* b = fdata(need(p, wname + ".bias"));
-    for (int o = 0; o < c.cout; ++o) shift[o] = b[o];
-  }
-  const float* w = fdata(wt);
   const int cin = c.cin, kh = c.kh, kw = c.kw, cp = c.cin_pad;
   c.prec = prec;
   auto folded = [&](int n, int k) -> float {
     const int cell = k / cp, ci = k % cp;
     if (ci >= cin) return 0.f;
     const int y = cell / kw, x = cell % kw;
-    return (float)((double)w[(((size_t)n * cin + ci) * kh + y) * kw + x] * scale[n]);
+    return f.w[(((size_t)n * cin + ci) * kh + y) * kw + x];
   };
   if (hilo) {
     c.krep = 2;
@@ -172,9 +202,7 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
     c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, folded);
   }
   c.wplane = (size_t)c.npad * c.kpad;
-  std::vector<float> bias(c.cout);
-  for (int o = 0; o < c.cout; ++o) bias[o] = (float)shift[o];
-  c.b = pack_vec(bias.data(), c.cout);
+  c.b = pack_vec(f.b.data(), c.cout);
   return c;
 }
 
@@ -349,6 +377,7 @@ void Model::build_resnet(const PMap& p) {
   const int cin_pad = stem_prec == Prec::F16 ? 8 : 4;
   stem_ = pack_conv(p, "conv1", "bn1", 2, cin_pad, stem_prec, eps_);
   if (stem_.kh != 7 || stem_.cin != 3) throw std::runtime_error("resnet stem must be 7x7 over 3 channels");
+  const FoldedConv stem_folded = fold_conv(p, "conv1", "bn1", eps_);
   for (int L = 1; L <= 4; ++L) {
     int nb = 0;
     while (has(p, "layer" + std::to_string(L) + "." + std::to_string(nb) + ".conv1.weight")) ++nb;
@@ -415,6 +444,19 @@ void Model::build_resnet(const PMap& p) {
     const ConvW* cs[] = {&b.c1, &b.c2, &b.c3, &b.ds};
     for (const ConvW* c : cs)
       if (c->cout && (c->cin_pad < 32 || c->cout % 32 != 0 || c->kh * c->kw > 31)) split_ = false;
+  }
+  // Fused stem (stem.hip: NCHW image -> conv + BN + ReLU -> max pool, one launch)
+  // for the fp16-activation modes and split fp16x3; fp32 keeps ingest + stem GEMM +
+  // max pool.  SPI_STEM_FUSED=0 selects the unfused path (A/B, tests).
+  const char* fe = std::getenv("SPI_STEM_FUSED");
+  const int stem_ow = (image_ + 6 - 7) / 2 + 1;
+  stem_fused_ = !(fe && *fe && std::atoi(fe) == 0) && stem_.cout == 64 && stem_.stride == 2 &&
+                stem_ow <= kStemPoolMaxOW && (prec_ == Prec::F16 || split_);
+  if (const char* e = std::getenv("SPI_STEM_PR"); e && *e) stem_pr_ = std::atoi(e) == 2 ? 2 : 1;
+  if (stem_fused_) {
+    std::vector<_Float16> packed(stem_pool_bytes() / sizeof(_Float16));
+    stem_pool_pack(stem_folded.w.data(), packed.data());
+    stem_pool_w_ = g_blob->add(packed.data(), stem_pool_bytes());
   }
 }
 
@@ -779,7 +821,7 @@ Workspace* Model::workspace(hipStream_t s) {
   std::vector<size_t> sizes;  // bytes per buffer
   if (family_ == SPI_FAMILY_RESNET) {
     const int cp = stem_.cin_pad;
-    sizes.push_back((size_t)B * image_ * image_ * cp * (stem_.prec == Prec::F16 ? 2 : 4));  // ingest
+    sizes.push_back(stem_fused_ ? 256 : (size_t)B * image_ * image_ * cp * (stem_.prec == Prec::F16 ? 2 : 4));  // ingest
     // F16M: the downsample outputs are fp32 in the same pool
     const size_t ea = mixed_ ? 4 : es;
     int H = image_, OH, OW;
@@ -787,8 +829,9 @@ Workspace* Model::workspace(hipStream_t s) {
     partial = std::max(partial, conv_partial(stem_, B, H, H));
     conv_desc(stem_, B, H, H, OH, OW);
     H = OH;
-    amax = std::max(amax, (size_t)B * H * H * stem_.cout);
+    if (!stem_fused_) amax = std::max(amax, (size_t)B * H * H * stem_.cout);  // else never materialised
     H = (H + 2 - 3) / 2 + 1;
+    amax = std::max(amax, (size_t)B * H * H * stem_.cout);
     for (const auto& b : blocks_) {
       int H2;
       if (b.has_ds)  // conv1 + downsample in one grouped launch (run_conv_pair)
@@ -863,7 +906,17 @@ Workspace* Model::workspace(hipStream_t s) {
 // graph-capturable) -> epilogue (writes the task's output buffer).
 // ---------------------------------------------------------------------------
 void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStream_t s) {
-  if (family_ == SPI_FAMILY_RESNET) {
+  if (family_ == SPI_FAMILY_RESNET && stem_fused_) {
+    // the stem reads the task's NCHW buffer itself and writes the pooled map (buf 2)
+    const int OH = (image_ + 6 - 7) / 2 + 1, PH = (OH + 2 - 3) / 2 + 1;
+    const int nrep = !prof_ ? 1
+                            : op_begin(s, "stem_pool", 2.0 * B * OH * OH * stem_.cout * 147.0,
+                                       (double)B * 3 * image_ * image_ * 4 + (double)B * PH * PH * stem_.cout * (split_ ? 4 : 2));
+    for (int r = 0; r < nrep; ++r)
+      stem_pool(static_cast<const float*>(in[0]), ptr<void>(stem_pool_w_), ptr<float>(stem_.b), w.bufs[2], B, image_,
+                image_, stem_.prec != Prec::F16, split_, stem_pr_, s);
+    if (prof_) op_end(s);
+  } else if (family_ == SPI_FAMILY_RESNET) {
     const int nrep = !prof_ ? 1 : op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);
     for (int r = 0; r < nrep; ++r)
       ingest_nchw(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, stem_.cin_pad,
@@ -890,18 +943,23 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
   if (family_ == SPI_FAMILY_RESNET) {
     int H = image_, OH, OW;
     void* const* buf = w.bufs.data();
-    run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w, s);
-    H = OH;
-    const int PH = (H + 2 - 3) / 2 + 1;
-    const int nrep = !prof_ ? 1 : op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
-    for (int r = 0; r < nrep; ++r) {
-      if (split_)
-        maxpool_nhwc_split(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, s);
-      else
-        maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+    if (stem_fused_) {  // stem + max pool ran in the prologue
+      OH = (H + 6 - 7) / 2 + 1;
+      H = (OH + 2 - 3) / 2 + 1;
+    } else {
+      run_conv(stem_, buf[0], B, H, H, buf[1], OH, OW, Act::Relu, nullptr, w, s);
+      H = OH;
+      const int PH = (H + 2 - 3) / 2 + 1;
+      const int nrep = !prof_ ? 1 : op_begin(s, "maxpool", 0, (double)B * (H * H + PH * PH) * stem_.cout * (f16_ ? 2 : 4));
+      for (int r = 0; r < nrep; ++r) {
+        if (split_)
+          maxpool_nhwc_split(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, s);
+        else
+          maxpool_nhwc(buf[1], buf[2], B, H, H, stem_.cout, PH, PH, 3, 2, 1, f16_, s);
+      }
+      if (prof_) op_end(s);
+      H = PH;
     }
-    if (prof_) op_end(s);
-    H = PH;
     int cur = 2;
     auto pick = [&](std::initializer_list<int> busy) {
       for (int i = 1; i <= 5; ++i)

@@ -155,6 +155,9 @@ class Model {
   bool bottleneck_ = false;
   std::vector<int> stage_blocks_;
   ConvW stem_;
+  bool stem_fused_ = false;  // stem + max pool in one launch on the NCHW input (stem.hip)
+  int stem_pr_ = 1;          // its pooled rows per workgroup (SPI_STEM_PR)
+  size_t stem_pool_w_ = 0;   // its weights, [hi | lo][64][24][8] fp16
   std::vector<ResBlock> blocks_;
   LinearW fc_;
   int image_ = 224, classes_ = 1000, feat_ = 512;

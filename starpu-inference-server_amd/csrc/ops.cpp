@@ -177,6 +177,25 @@ int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, i
   return check_launch();
 }
 
+size_t spi_op_stem_pool_bytes(void) { return spi::stem_pool_bytes(); }
+
+int spi_op_stem_pool_pack(const float* w, void* dst) {
+  if (!w || !dst) return fail("invalid stem_pool pack arguments");
+  spi::stem_pool_pack(w, static_cast<_Float16*>(dst));
+  return 0;
+}
+
+int spi_op_stem_pool(int32_t precision, const float* x, int32_t B, int32_t H, int32_t W, const void* Wp,
+                     const float* bias, void* y, int32_t rows_per_block, void* stream) {
+  if (precision < 1 || precision > 3 || !x || !Wp || !bias || !y || B <= 0 || H <= 0 || W <= 0 ||
+      rows_per_block < 0 || rows_per_block > 2)
+    return fail("invalid stem_pool arguments");
+  if ((W + 6 - 7) / 2 + 1 > spi::kStemPoolMaxOW) return fail("stem_pool: image wider than 224");
+  spi::stem_pool(x, Wp, bias, y, B, H, W, precision >= 2, precision == 3, rows_per_block ? rows_per_block : 1,
+                 static_cast<hipStream_t>(stream));
+  return check_launch();
+}
+
 int spi_op_attention(int32_t precision, const void* qkv, const float* mask_bias, void* ctx, int32_t B, int32_t S,
                      int32_t heads, float scale, void* stream) {
   if ((precision != 0 && precision != 1) || !qkv || !ctx || B <= 0 || S <= 0 || heads <= 0)

@@ -81,6 +81,16 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
                  bool f16, hipStream_t s);
+// Fused ResNet stem (stem.hip): NCHW fp32 image [B][3][H][W] -> 7x7/s2/p3 conv
+// (64 output channels, folded BN) + ReLU -> 3x3/s2/p1 max pool -> NHWC [B][PH][PW][64]:
+// fp16 (split false) or the split layout (split true, needs lo).  lo: hi + lo
+// weights and image (three fp16 MFMAs per fragment, fp32-grade); else fp16 only.
+// w: stem_pool_bytes() from stem_pool_pack(); pr: pooled rows per workgroup (1, 2).
+constexpr int kStemPoolMaxOW = 112;  // stem output width bound (images up to 224)
+constexpr size_t stem_pool_bytes() { return (size_t)2 * 64 * 24 * 8 * sizeof(_Float16); }
+void stem_pool_pack(const float* w_folded /* [64][3][7][7] */, _Float16* dst);
+void stem_pool(const float* x, const void* w, const float* bias, void* y, int B, int H, int W, bool lo,
+               bool split, int pr, hipStream_t s);
 // 3x3/s2/p1 max pool on NHWC.
 void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH,
                   int OW, int k, int stride, int pad, bool f16, hipStream_t s);

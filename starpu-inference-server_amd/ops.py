@@ -132,3 +132,26 @@ def avgpool_fc(prec, x, W_packed, N_, bias=None, act=None, ws=None, stream=None)
     _check(lib.spi_op_avgpool_fc(PREC[prec], _ptr(x), B, HW, Cc, _ptr(W_packed), N_, _ptr(bias), _ptr(out), ACT[act],
                                  _ptr(ws), C.c_void_p(s)))
     return out
+
+
+STEM_PREC = {"fp16": 1, "fp16m": 2, "fp16x3s": 3}  # fp16 operands / hi+lo operands, fp16 out / ... split out
+
+
+def stem_pool(prec, x_nchw, w_folded, bias, rows_per_block=0, stream=None):
+    """Fused ResNet stem (7x7/s2 conv over 3 channels, 64 out, folded BN bias, ReLU, 3x3/s2 max pool)
+    on the NCHW fp32 image, one launch.  Returns NHWC [B][PH][PW][64]: fp16, or for fp16x3s the split
+    layout in a float32-storage tensor."""
+    B, _, H, W_ = x_nchw.shape
+    oh, ow = (H - 1) // 2 + 1, (W_ - 1) // 2 + 1
+    ph, pw = (oh - 1) // 2 + 1, (ow - 1) // 2 + 1
+    w = np.ascontiguousarray(np.asarray(w_folded.cpu() if isinstance(w_folded, torch.Tensor) else w_folded,
+                                        dtype=np.float32))
+    host = np.empty(lib.spi_op_stem_pool_bytes(), dtype=np.uint8)
+    _check(lib.spi_op_stem_pool_pack(w.ctypes.data, host.ctypes.data))
+    wp = torch.from_numpy(host).to(x_nchw.device)
+    out = torch.empty(B, ph, pw, 64, device=x_nchw.device,
+                      dtype=torch.float32 if prec == "fp16x3s" else torch.float16)
+    s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+    _check(lib.spi_op_stem_pool(STEM_PREC[prec], _ptr(x_nchw), B, H, W_, _ptr(wp), _ptr(bias), _ptr(out),
+                                rows_per_block, C.c_void_p(s)))
+    return out

@@ -287,3 +287,33 @@ def test_gemm_256x128_eight_waves(ops, big_tiles, prec, M, N, K):
     out = ops.gemm(prec, A_in.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda())
     err = normalized_max_error(out.cpu().numpy(), ref.numpy())
     assert err < TOL[prec], f"{prec} {M}x{N}x{K}: {err:.3e}"
+
+
+def stem_pool_ref(x, w, b):
+    """torchvision's conv1 (BN folded into w / b) + relu + maxpool, fp32."""
+    return F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp16m", "fp16x3s"])
+@pytest.mark.parametrize("B,H,W,rows", [(8, 224, 224, 0), (8, 224, 224, 2), (3, 64, 64, 0), (1, 65, 47, 0),
+                                        (2, 33, 17, 2), (1, 9, 9, 0), (2, 223, 224, 1)])
+def test_stem_pool_fused(ops, prec, B, H, W, rows):
+    """Fused stem (NCHW fp32 image -> 7x7/s2 conv + bias + ReLU -> 3x3/s2 max pool, one launch)
+    vs F.conv2d / relu / max_pool2d: odd sizes exercise the partial column blocks, the pool's
+    edge windows and a last workgroup with fewer pooled rows than rows_per_block."""
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + W + rows)
+    x = torch.rand(B, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    b = torch.randn(64, generator=g) * 0.1
+    if prec == "fp16":
+        ref = stem_pool_ref(x.half().float(), w.half().float(), b)
+    else:
+        ref = stem_pool_ref(x.double(), w.double(), b.double()).float()
+    out = ops.stem_pool(prec, x.cuda(), w, b.cuda(), rows_per_block=rows)
+    torch.cuda.synchronize()
+    got = ops.from_split(out.cpu()) if prec == "fp16x3s" else out.float().cpu()
+    assert got.shape == ref.shape
+    err = normalized_max_error(got.numpy(), ref.numpy())
+    # fp16 / fp16m store fp16 (relative 2^-11); fp16x3s stores hi + lo (~2^-22)
+    tol = 1e-5 if prec == "fp16x3s" else 1e-3
+    assert err < tol, f"stem_pool {prec} {B}x{H}x{W}: {err:.3e}"

@@ -206,3 +206,21 @@ def test_hip_matches_committed_golden_fixtures(spi, gpu, name, prec):
     tol = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16": 1e-3 if name.startswith("bert") else TOL_RESNET_PLAIN_FP16}[prec]
     print(f"golden {name} {prec} err={err:.3e}")
     assert err < tol
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp16x3", "fp16m"])
+def test_resnet18_fused_stem_matches_unfused(spi, zoo, gpu, prec, monkeypatch):
+    """The fused stem (one launch on the NCHW input) against the ingest + stem GEMM + max pool
+    path (SPI_STEM_FUSED=0) on the same replica weights: the same numbers up to the
+    accumulation order of the 147-term stem dot products."""
+    rng = np.random.default_rng(5)
+    m = zoo.resnet18(image=224)
+    x = image(rng, 2, 224)
+    ref = cpu_inference(m, [x])[0]
+    fused = hip_forward(spi, spi.ModelReplica(m, 0, prec, max_batch=2), [x], ref.shape)
+    monkeypatch.setenv("SPI_STEM_FUSED", "0")
+    unfused = hip_forward(spi, spi.ModelReplica(m, 0, prec, max_batch=2), [x], ref.shape)
+    d = normalized_max_error(fused, unfused)
+    print(f"resnet18 {prec} fused vs unfused stem: {d:.3e}, vs oracle {normalized_max_error(fused, ref):.3e}")
+    assert d < (1e-5 if prec == "fp16x3" else 1e-3)
+    assert normalized_max_error(fused, ref) < resnet_tol(prec)
