@@ -274,11 +274,13 @@ def test_gemm_256x128_eight_waves(ops, big_tiles, prec, M, N, K):
     W = torch.randn(N, K, generator=g) / K ** 0.5
     b = torch.randn(N, generator=g)
     if prec == "fp16x3s":
+        if N % 32:
+            pytest.skip("the split layout needs N a multiple of 32")
         As = ops.to_split(A)
         ref = ops.from_split(As) @ W.T + b
-        out = ops.gemm(prec, As.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda())
-        got = ops.from_split(out.cpu()) if out.dtype != torch.float32 or out.shape[1] != N else out.cpu()
-        err = normalized_max_error(got.numpy(), ref.numpy())
+        out = ops.gemm(prec, As.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda(),
+                       out=torch.empty(M, N, device="cuda"))
+        err = normalized_max_error(ops.from_split(out.cpu()).numpy(), ref.numpy())
         assert err < 1e-5
         return
     dt = ops.act_dtype(prec)
