@@ -1130,6 +1130,7 @@ struct Knobs {
   int halo_stages = 3, halo_minh = 14;
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
   int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
+  int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
   int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
@@ -1166,6 +1167,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_BIG"); e && *e) k.big = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
     // (OW 0 = any other width; rows 0 = not a halo conv)
@@ -1563,7 +1565,10 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   check_desc(d, prec);
   switch (prec) {
     case Prec::F16:
-      launch<(int)Prec::F16>(d, p, s);
+      if (gemm256_eligible(d, prec, knobs().g256_min))
+        gemm256(d, p, s);
+      else
+        launch<(int)Prec::F16>(d, p, s);
       break;
     case Prec::F32:
       launch<(int)Prec::F32>(d, p, s);

@@ -78,6 +78,12 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s);
 void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, Prec prec,
                hipStream_t s);
 
+// 256x256-tile 8-wave fp16 GEMM (gemm256.hip) for large dense F16 contractions;
+// gemm() routes a desc to it when gemm256_eligible (N % 256 == 0, K % 64 == 0,
+// at least min_tiles 256^2 tiles; SPI_GEMM_256_MIN, default 128, 0 = never).
+bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
+void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
+
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
                  bool f16, hipStream_t s);

@@ -319,3 +319,57 @@ def test_stem_pool_fused(ops, prec, B, H, W, rows):
     # fp16 / fp16m store fp16 (relative 2^-11); fp16x3s stores hi + lo (~2^-22)
     tol = 1e-5 if prec == "fp16x3s" else 1e-3
     assert err < tol, f"stem_pool {prec} {B}x{H}x{W}: {err:.3e}"
+
+
+@pytest.fixture
+def gemm256_everywhere(ops):
+    import os
+    os.environ["SPI_GEMM_256_MIN"] = "1"
+    ops.lib.spi_debug_gemm_reload_env()
+    yield
+    os.environ.pop("SPI_GEMM_256_MIN", None)
+    ops.lib.spi_debug_gemm_reload_env()
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 256, 64), (300, 512, 128), (256, 768, 192), (1000, 1024, 640),
+                                   (3152, 1024, 4096)])
+@pytest.mark.parametrize("act,res,out_f32", [(None, None, True), ("gelu", None, False), ("relu", "f16", False),
+                                             (None, "f32", True)])
+def test_gemm256_tiles(ops, gemm256_everywhere, M, N, K, act, res, out_f32):
+    """The 256x256 8-wave phased GEMM (gemm256.hip; SPI_GEMM_256_MIN=1 routes every eligible
+    fp16 GEMM to it): one k-tile (the peeled last tile only), ragged M, bias / GELU / ReLU,
+    fp16 and fp32 residuals, fp16 and fp32 outputs."""
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    A = torch.randn(M, K, generator=g).half()
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = None
+    if res:
+        R = torch.randn(M, N, generator=g)
+        R = R.half() if res == "f16" else R
+    ref = A.float() @ W.half().float().T + b
+    if R is not None:
+        ref = ref + R.float()
+    if act == "gelu":
+        ref = F.gelu(ref)
+    elif act == "relu":
+        ref = F.relu(ref)
+    out = ops.gemm("fp16", A.cuda(), ops.pack_weight("fp16", W), N, bias=b.cuda(),
+                   residual=None if R is None else R.cuda(), out_f32=out_f32, act=act)
+    torch.cuda.synchronize()
+    err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
+    assert err < (1e-5 if out_f32 else 2e-3), f"gemm256 {M}x{N}x{K} {act} {res}: {err:.3e}"
+
+
+def test_gemm256_unaligned_output(ops, gemm256_everywhere):
+    """An output buffer off 16-byte alignment takes gemm256's per-element epilogue."""
+    M, N, K = 300, 512, 128
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn(M, K, generator=g).half()
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    ref = F.gelu(A.float() @ W.half().float().T + b)
+    out = torch.empty(M * N + 1, device="cuda", dtype=torch.float16)[1:].view(M, N)
+    ops.gemm("fp16", A.cuda(), ops.pack_weight("fp16", W), N, bias=b.cuda(), out=out, out_f32=False, act="gelu")
+    torch.cuda.synchronize()
+    assert normalized_max_error(out.float().cpu().numpy(), ref.numpy()) < 2e-3
