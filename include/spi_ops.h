@@ -64,7 +64,8 @@ int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, i
  * precision 1: fp16 operands, fp16 y; 2: hi + lo fp16 operands (fp32-grade), fp16 y
  * (the fp16m stem); 3: as 2 with y in the split layout.  W_packed: spi_op_stem_pool_bytes()
  * of device memory filled from spi_op_stem_pool_pack(w_host fp32 [64][3][7][7]).
- * rows_per_block: pooled rows per workgroup (0 = default 1, or 2).  W <= 224. */
+ * rows_per_block: 0 = default (2 pooled rows per 8-wave workgroup for maps wider than 64,
+ * else 1 per 4 waves), 1 or 2 = that many per 4-wave workgroup.  W <= 224. */
 size_t spi_op_stem_pool_bytes(void);
 int spi_op_stem_pool_pack(const float* w_host, void* dst_host);
 int spi_op_stem_pool(int32_t precision, const float* x, int32_t B, int32_t H, int32_t W,

@@ -452,7 +452,7 @@ void Model::build_resnet(const PMap& p) {
   const int stem_ow = (image_ + 6 - 7) / 2 + 1;
   stem_fused_ = !(fe && *fe && std::atoi(fe) == 0) && stem_.cout == 64 && stem_.stride == 2 &&
                 stem_ow <= kStemPoolMaxOW && (prec_ == Prec::F16 || split_);
-  if (const char* e = std::getenv("SPI_STEM_PR"); e && *e) stem_pr_ = std::atoi(e) == 2 ? 2 : 1;
+  if (const char* e = std::getenv("SPI_STEM_PR"); e && *e) stem_pr_ = std::atoi(e);  // 1 / 2: 4-wave variants
   if (stem_fused_) {
     std::vector<_Float16> packed(stem_pool_bytes() / sizeof(_Float16));
     stem_pool_pack(stem_folded.w.data(), packed.data());

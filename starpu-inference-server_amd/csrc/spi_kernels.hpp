@@ -91,7 +91,7 @@ void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
 // (64 output channels, folded BN) + ReLU -> 3x3/s2/p1 max pool -> NHWC [B][PH][PW][64]:
 // fp16 (split false) or the split layout (split true, needs lo).  lo: hi + lo
 // weights and image (three fp16 MFMAs per fragment, fp32-grade); else fp16 only.
-// w: stem_pool_bytes() from stem_pool_pack(); pr: pooled rows per workgroup (1, 2).
+// w: stem_pool_bytes() from stem_pool_pack(); pr: 0 auto, 1 / 2 pooled rows per 4-wave workgroup.
 constexpr int kStemPoolMaxOW = 112;  // stem output width bound (images up to 224)
 constexpr size_t stem_pool_bytes() { return (size_t)2 * 64 * 24 * 8 * sizeof(_Float16); }
 void stem_pool_pack(const float* w_folded /* [64][3][7][7] */, _Float16* dst);

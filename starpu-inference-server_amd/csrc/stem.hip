@@ -48,6 +48,7 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kCout = 64;
 constexpr int kGroups = 24;  // (c, kh) groups of 8 kw values: 21 real + 3 zero
@@ -59,34 +60,40 @@ struct Geom {
   static constexpr int NR = 2 * R + 5;  // input rows per workgroup
   static constexpr int WP = 256;        // plane width (fp16): columns -3 .. 2 kStemPoolMaxOW + 4, 512 B
   static constexpr int NPL = 3 * NR;    // planes (channel, input row)
-  // + slack: the last group's rows past the map read up to 32 dwords beyond the last plane
-  static constexpr int LDS_HALF = NPL * WP + 64;
+  // one plane image in dwords, + slack: the last group's rows past the map read up to
+  // 32 dwords beyond the last plane
+  static constexpr int PD = NPL * WP / 2 + 32;
 };
 static_assert(2 * kStemPoolMaxOW + 5 < Geom<1>::WP, "plane covers the valid windows");
 
+// phase PH_'s fragment from an 8-dword block pair: dwords (PH_ & 2) .. (PH_ & 2) + 3
 template <int PH_>
-__device__ __forceinline__ half8 window(const u32x4& b0, const u32x4& b1) {
-  u32x4 r;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) r[q] = PH_ + q < 4 ? b0[(PH_ + q) & 3] : b1[(PH_ + q) & 3];
-  return __builtin_bit_cast(half8, r);
+__device__ __forceinline__ half8 window(const u32x8& b) {
+  if constexpr (PH_ & 2)
+    return __builtin_bit_cast(half8, __builtin_shufflevector(b, b, 2, 3, 4, 5));
+  else
+    return __builtin_bit_cast(half8, __builtin_shufflevector(b, b, 0, 1, 2, 3));
 }
 
 // OUT 0: fp16 NHWC [B][PH][PW][64]; 1: split NHWC (per pixel [32 hi | 32 lo] x 2).
-template <int PR, bool LO, int OUT>
-__global__ __launch_bounds__(256) void stem_pool_kernel(const float* __restrict__ x, const _Float16* __restrict__ w,
-                                                        const float* __restrict__ bias, void* __restrict__ y, int H,
-                                                        int W, int OH, int OW, int PH, int PW, int diag) {
+template <int PR, int NW, bool LO, int OUT>
+__global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restrict__ x, const _Float16* __restrict__ w,
+                                                            const float* __restrict__ bias, void* __restrict__ y, int H,
+                                                            int W, int OH, int OW, int PH, int PW, int diag) {
   using G = Geom<PR>;
-  constexpr int R = G::R, NR = G::NR, WP = G::WP, NPL = G::NPL, LH = G::LDS_HALF;
-  __shared__ __attribute__((aligned(16))) _Float16 lds[(LO ? 2 : 1) * LH];
+  constexpr int R = G::R, NR = G::NR, WP = G::WP, NPL = G::NPL, PD = G::PD, NT = 64 * NW;
+  static_assert(NW == 4 || NW == 8, "4 waves (one per 16 channels), or 8 (x 2 pixel groups)");
+  static_assert(NW == 4 || kStemPoolMaxOW <= 128, "8 waves: one 64-pixel group per wave");
+  // images: [copy 0 hi | copy 1 hi | copy 0 lo | copy 1 lo], copy 1 = copy 0 shifted one dword
+  __shared__ __attribute__((aligned(16))) unsigned lds[(LO ? 4 : 2) * PD];
+  __shared__ float xch[NW == 8 ? 2 * PR * kCout : 1];  // 8 waves: group 0's last column per pooled row
   const int b = blockIdx.y;
   const int pr0 = blockIdx.x * PR;
   const int sr0 = 2 * pr0 - 1;  // first stem row (the pool's padding row for pr0 = 0)
   const int ir0 = 2 * sr0 - 3;  // first input row
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int n = wave * 16 + fr;
+  const int n = (wave & 3) * 16 + fr;
 
   // weights first: L2-resident, their latency overlaps the plane fill
   half8 wh[kSteps], wl[kSteps];
@@ -103,11 +110,11 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const float* __restrict_
   // the image.  Unrolled: every thread's loads are in flight before the first LDS
   // store (a rolled loop waits out one memory latency per iteration).
   const float* xb = x + (size_t)b * 3 * H * W;
-  constexpr int HALF = WP / 2, ITER = (NPL * HALF + 255) / 256;
+  constexpr int HALF = WP / 2, ITER = (NPL * HALF + NT - 1) / NT;
   float v[ITER][2];
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
-    const int e = tid + it * 256;
+    const int e = tid + it * NT;
     const int p = e / HALF, i = (e - p * HALF) * 2;
     const int c = p / NR, r = ir0 + (p - c * NR);
     v[it][0] = v[it][1] = 0.f;
@@ -118,22 +125,33 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const float* __restrict_
       if (c0 + 1 >= 0 && c0 + 1 < W) v[it][1] = row[c0 + 1];
     }
   }
-  unsigned* ldw = reinterpret_cast<unsigned*>(lds);
+  unsigned* ldw = lds;
+  auto pack2 = [](_Float16 a, _Float16 b) {
+    return __builtin_bit_cast(unsigned short, a) | (unsigned)__builtin_bit_cast(unsigned short, b) << 16;
+  };
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
-    const int e = tid + it * 256;
+    const int e = tid + it * NT;
     if (e >= NPL * HALF) continue;
     const _Float16 h0 = static_cast<_Float16>(v[it][0]), h1 = static_cast<_Float16>(v[it][1]);
-    ldw[e] = __builtin_bit_cast(unsigned short, h0) | (unsigned)__builtin_bit_cast(unsigned short, h1) << 16;
+    const unsigned hw = pack2(h0, h1);
+    ldw[e] = hw;
+    if (e) ldw[PD + e - 1] = hw;
     if constexpr (LO) {
-      const _Float16 l0 = static_cast<_Float16>(v[it][0] - static_cast<float>(h0));
-      const _Float16 l1 = static_cast<_Float16>(v[it][1] - static_cast<float>(h1));
-      ldw[LH / 2 + e] = __builtin_bit_cast(unsigned short, l0) | (unsigned)__builtin_bit_cast(unsigned short, l1) << 16;
+      const unsigned lw = pack2(static_cast<_Float16>(v[it][0] - static_cast<float>(h0)),
+                                static_cast<_Float16>(v[it][1] - static_cast<float>(h1)));
+      ldw[2 * PD + e] = lw;
+      if (e) ldw[3 * PD + e - 1] = lw;
     }
   }
-  if (tid < 32) {  // the slack after the last plane: finite bytes for the discarded rows
-    ldw[NPL * HALF + tid] = 0u;
-    if constexpr (LO) ldw[LH / 2 + NPL * HALF + tid] = 0u;
+  if (tid < 33) {  // the slack after the last plane: finite bytes for the discarded rows
+#pragma unroll
+    for (int c = 0; c < (LO ? 4 : 2); ++c) {
+      if (c & 1)
+        ldw[c * PD + NPL * HALF - 1 + tid] = 0u;  // copy 1: its last dword is copy 0's first slack dword
+      else if (tid < 32)
+        ldw[c * PD + NPL * HALF + tid] = 0u;
+    }
   }
   __syncthreads();
 
@@ -146,85 +164,85 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const float* __restrict_
     goff[s] = (c * NR + kh) * HALF;
   }
 
-  float carry[PR];
-#pragma unroll
-  for (int p = 0; p < PR; ++p) carry[p] = 0.f;
   const int NG = diag == 2 ? 0 : (OW + 63) >> 6;  // diagnostic 2: fill only
-  for (int grp = 0; grp < NG; ++grp) {
+  // Stem rows of one 64-pixel group, folded as they complete (bias + ReLU, invalid
+  // pixels as 0) into the vertical max of each pooled row; lane column t = 4 v + ph
+  // is stem column 64 grp + 16 fq + t.
+  auto compute = [&](int grp, float (&vm)[PR][16]) {
     const int blk = grp * 64 + 4 * fr;  // dword of this lane's first block
-    floatx4 acc[R][4];
+    const int o0 = grp * 64 + 16 * fq;
+    float bt[16];  // bias per lane column; -inf past the map, so ReLU sends those to 0
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int t = 0; t < 16; ++t) bt[t] = o0 + t < OW ? bn : -__builtin_inff();
 #pragma unroll
-      for (int ph = 0; ph < 4; ++ph) acc[r][ph] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // (k-step, stem row) steps, software-pipelined: step t + 1's four blocks are
-    // read before step t's twelve (split) / four MFMAs are issued, so the LDS
-    // latency hides behind the MFMAs of the same wave
+    for (int p = 0; p < PR; ++p)
+#pragma unroll
+      for (int t = 0; t < 16; ++t) vm[p][t] = 0.f;
+    floatx4 acc[4];
+    // (stem row, k-step) steps, software-pipelined: step t + 1's blocks are read
+    // before step t's twelve (split) / four MFMAs are issued.  A step reads dwords
+    // [4 i, 4 i + 8) of copy 0 and of copy 1 (copy 0 shifted one dword) as 8-dword
+    // vectors (two ds_read_b128 each, consecutive registers): phase 0 / 2 windows are
+    // dwords 0-3 / 2-5 of copy 0, phase 1 / 3 the same of copy 1 -- even-aligned
+    // register sub-ranges, so no window needs a register move.
     constexpr int T = kSteps * R;
-    u32x4 blk_[2][4];
-    auto load = [&](int t, u32x4(&dst)[4]) {
-      const int s = t / R, r = t - s * R;
-      const u32x4* src = reinterpret_cast<const u32x4*>(ldw + goff[s] + r * WP + blk);
-      dst[0] = src[0];
-      dst[1] = src[1];
-      if constexpr (LO) {
-        dst[2] = src[LH / 8];
-        dst[3] = src[LH / 8 + 1];
-      }
+    constexpr int NB = LO ? 4 : 2;
+    u32x8 blk_[2][NB];
+    auto load = [&](int t, u32x8(&dst)[NB]) {
+      const int r = t / kSteps, s = t - r * kSteps;
+      const unsigned* src = ldw + goff[s] + r * WP + blk;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) dst[c] = *reinterpret_cast<const u32x8*>(src + c * PD);
     };
     load(0, blk_[0]);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const int s = t / R, r = t - s * R;
+      const int r = t / kSteps, s = t - r * kSteps;
+      if (s == 0)
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) acc[ph] = floatx4{0.f, 0.f, 0.f, 0.f};
       if (t + 1 < T) load(t + 1, blk_[(t + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      const u32x4(&bb)[4] = blk_[t & 1];
+      const u32x8(&bb)[NB] = blk_[t & 1];
       auto mma = [&](auto phc) {
         constexpr int P = decltype(phc)::value;
-        const half8 ah = window<P>(bb[0], bb[1]);
+        const half8 ah = window<P>(bb[P & 1]);
         if constexpr (LO) {
-          const half8 al = window<P>(bb[2], bb[3]);
-          acc[r][P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh[s], acc[r][P], 0, 0, 0);
-          acc[r][P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl[s], acc[r][P], 0, 0, 0);
+          const half8 al = window<P>(bb[2 + (P & 1)]);
+          acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh[s], acc[P], 0, 0, 0);
+          acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl[s], acc[P], 0, 0, 0);
         }
-        acc[r][P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh[s], acc[r][P], 0, 0, 0);
+        acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh[s], acc[P], 0, 0, 0);
       };
       mma(std::integral_constant<int, 0>{});
       mma(std::integral_constant<int, 1>{});
       mma(std::integral_constant<int, 2>{});
       mma(std::integral_constant<int, 3>{});
       __builtin_amdgcn_sched_barrier(0);
+      // row r complete: fold it into the pooled rows it belongs to (rows outside the
+      // map skipped -- a wave-uniform test; columns past the map carry a -inf bias)
+      if (s == kSteps - 1 && sr0 + r >= 0 && sr0 + r < OH) {
+#pragma unroll
+        for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph) {
+            const int tt = 4 * vv + ph;
+            const float u = acc[ph][vv] + bt[tt];
+#pragma unroll
+            for (int p = 0; p < PR; ++p)
+              if (r >= 2 * p && r <= 2 * p + 2) vm[p][tt] = __builtin_fmaxf(__builtin_fmaxf(vm[p][tt], u), 0.f);
+          }
+      }
     }
-    // bias + ReLU, vertical max per pooled row (invalid stem pixels enter as 0);
-    // lane column t = 4 v + ph is stem column o0 + t
+  };
+  // horizontal: pooled columns o0 / 2 + q, q = 0..7 (stem columns o0 + 2q - 1 .. o0 + 2q + 1);
+  // column o0 - 1 from lane - 16, or for the first lane group `first` (the previous group's last)
+  auto store = [&](int grp, const float (&vm)[PR][16], const float (&first)[PR]) {
     const int o0 = grp * 64 + 16 * fq;
-    float vm[PR][16];
-#pragma unroll
-    for (int p = 0; p < PR; ++p)
-#pragma unroll
-      for (int t = 0; t < 16; ++t) vm[p][t] = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool rv = sr0 + r >= 0 && sr0 + r < OH;
-#pragma unroll
-      for (int vv = 0; vv < 4; ++vv)
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-          const int t = 4 * vv + ph;
-          const float u = acc[r][ph][vv] + bn;
-          const float val = rv && o0 + t < OW && u > 0.f ? u : 0.f;
-#pragma unroll
-          for (int p = 0; p < PR; ++p)
-            if (r >= 2 * p && r <= 2 * p + 2) vm[p][t] = fmaxf(vm[p][t], val);
-        }
-    }
-    // horizontal: pooled columns o0 / 2 + q, q = 0..7 (stem columns o0 + 2q - 1 .. o0 + 2q + 1);
-    // column o0 - 1 from lane - 16, or for the first lane group the previous group's last
 #pragma unroll
     for (int p = 0; p < PR; ++p) {
       float left = __shfl_up(vm[p][15], 16, 64);
-      if (fq == 0) left = carry[p];
-      carry[p] = __shfl(vm[p][15], 48 + fr, 64);
+      if (fq == 0) left = first[p];
       const int pr = pr0 + p;
       if (pr >= PH) continue;
       const size_t m0 = ((size_t)b * PH + pr) * PW;
@@ -244,23 +262,51 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(const float* __restrict_
         }
       }
     }
+  };
+  float vm[PR][16];
+  if constexpr (NW == 4) {  // one wave walks every group, carrying the boundary column
+    float carry[PR];
+#pragma unroll
+    for (int p = 0; p < PR; ++p) carry[p] = 0.f;
+    for (int grp = 0; grp < NG; ++grp) {
+      compute(grp, vm);
+      store(grp, vm, carry);
+#pragma unroll
+      for (int p = 0; p < PR; ++p) carry[p] = __shfl(vm[p][15], 48 + fr, 64);
+    }
+  } else {  // waves 0-3 group 0, waves 4-7 group 1; group 0's last column through LDS
+    const int grp = wave >> 2;
+    const bool active = grp < NG;
+    if (active) {
+      compute(grp, vm);
+      if (grp == 0 && fq == 3)
+#pragma unroll
+        for (int p = 0; p < PR; ++p) xch[p * kCout + n] = vm[p][15];
+    }
+    __syncthreads();
+    if (active) {
+      float first[PR];
+#pragma unroll
+      for (int p = 0; p < PR; ++p) first[p] = grp ? xch[p * kCout + n] : 0.f;
+      store(grp, vm, first);
+    }
   }
 }
 
-template <int PR>
+template <int PR, int NW>
 void launch_pr(const float* x, const _Float16* w, const float* bias, void* y, int B, int H, int W, int OH, int OW,
                int PH, int PW, bool lo, bool split, hipStream_t s) {
   static const int diag = [] {
     const char* e = std::getenv("SPI_STEM_DIAG");  // 1: no image loads, 2: fill only, 3: empty
     return e && *e ? std::atoi(e) : 0;
   }();
-  const dim3 grid((PH + PR - 1) / PR, B);
+  const dim3 grid((PH + PR - 1) / PR, B), block(64 * NW);
   if (split)
-    hipLaunchKernelGGL((stem_pool_kernel<PR, true, 1>), grid, dim3(256), 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, true, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
   else if (lo)
-    hipLaunchKernelGGL((stem_pool_kernel<PR, true, 0>), grid, dim3(256), 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, true, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
   else
-    hipLaunchKernelGGL((stem_pool_kernel<PR, false, 0>), grid, dim3(256), 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, false, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
 }
 
 }  // namespace
@@ -285,10 +331,14 @@ void stem_pool(const float* x, const void* w, const float* bias, void* y, int B,
   if (OW > kStemPoolMaxOW || OH < 1 || OW < 1 || B < 1) throw std::runtime_error("stem_pool: unsupported image size");
   if (split && !lo) throw std::runtime_error("stem_pool: split output needs split weights");
   const _Float16* wp = static_cast<const _Float16*>(w);
+  // pr: 1 / 2 pooled rows per 4-wave workgroup; 0 (default): two rows per 8-wave
+  // workgroup (one 64-pixel group per wave) when the map has two groups, else 1 x 4 waves
   if (pr == 2)
-    launch_pr<2>(x, wp, bias, y, B, H, W, OH, OW, PH, PW, lo, split, s);
+    launch_pr<2, 4>(x, wp, bias, y, B, H, W, OH, OW, PH, PW, lo, split, s);
+  else if (pr == 1 || OW <= 64)
+    launch_pr<1, 4>(x, wp, bias, y, B, H, W, OH, OW, PH, PW, lo, split, s);
   else
-    launch_pr<1>(x, wp, bias, y, B, H, W, OH, OW, PH, PW, lo, split, s);
+    launch_pr<2, 8>(x, wp, bias, y, B, H, W, OH, OW, PH, PW, lo, split, s);
 }
 
 }  // namespace spi

@@ -25,7 +25,7 @@ s = torch.cuda.current_stream().cuda_stream
 flops = 2.0 * B * 112 * 112 * 64 * 147
 only = os.environ.get("STEM_ONLY")  # e.g. "fp16m:1"
 for prec, name in [(1, "fp16"), (2, "fp16m"), (3, "fp16x3s")]:
-    for rows in (1, 2):
+    for rows in (0, 1, 2):
         if only and only != f"{name}:{rows}":
             continue
         call = lambda: lib.spi_op_stem_pool(prec, ops._ptr(x), B, 224, 224, ops._ptr(wp), ops._ptr(b), ops._ptr(y),
