@@ -371,6 +371,8 @@ def main():
                     help="default: the parity-grade fp16 mode of the model (DEFAULT_PRECISION)")
     ap.add_argument("--workers", type=int, default=4, help="worker streams per GPU")
     ap.add_argument("--tasks-per-step", type=int, default=8, help="codelet calls per worker per step")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="re-time the same K-step region this many times after `value` (value_repeats)")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline budget per layout (0 = skip)")
     ap.add_argument("--e2e-requests", type=int, default=4000)
@@ -423,6 +425,9 @@ def main():
     elapsed = h.throughput(args.steps, args.warmup, args.tasks_per_step, world, dist)
     per_step = args.workers * args.tasks_per_step * args.batch
     value = world * per_step * args.steps / elapsed
+    # stability evidence: the same K-step region re-timed (not `value`, which is the first region)
+    repeats = [world * per_step * args.steps / h.throughput(args.steps, 0, args.tasks_per_step, world, dist)
+               for _ in range(args.repeats)]
     task_lat = h.loaded_latency(20)
 
     result = {
@@ -454,6 +459,7 @@ def main():
             "hip_hw_queues": queues,
             "parallelism": f"replicas x{world} (request sharding, no collective)",
         },
+        "value_repeats": [round(v, 1) for v in repeats],
         "p50_task_latency_ms": round(percentile(task_lat, 50), 4),
         "p95_task_latency_ms": round(percentile(task_lat, 95), 4),
     }
