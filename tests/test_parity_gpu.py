@@ -224,3 +224,13 @@ def test_resnet18_fused_stem_matches_unfused(spi, zoo, gpu, prec, monkeypatch):
     print(f"resnet18 {prec} fused vs unfused stem: {d:.3e}, vs oracle {normalized_max_error(fused, ref):.3e}")
     assert d < (1e-5 if prec == "fp16x3" else 1e-3)
     assert normalized_max_error(fused, ref) < resnet_tol(prec)
+
+
+def test_resnet18_wide_image_unfused_stem(spi, zoo, gpu):
+    """Images wider than 224 (stem output > 112 columns) take the ingest + stem GEMM + max pool path."""
+    rng = np.random.default_rng(9)
+    m = zoo.resnet18(image=240)
+    x = image(rng, 1, 240)
+    ref = cpu_inference(m, [x])[0]
+    got = hip_forward(spi, spi.ModelReplica(m, 0, "fp16m", max_batch=1, image_size=240), [x], ref.shape)
+    assert normalized_max_error(got, ref) < TOL_RESNET_PLAIN_FP16
