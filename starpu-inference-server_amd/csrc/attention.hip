@@ -69,22 +69,38 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv,
     o[r] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
 
-  for (int k0 = 0; k0 < S; k0 += KT) {
-    __syncthreads();
-    for (int c = tid; c < KT * HD / EPC; c += 256) {
+  // K / V tiles go through registers one tile ahead: tile t + 1's global loads are in
+  // flight while tile t computes.  Raw barriers (LDS wait + s_barrier): a
+  // __syncthreads() fence would also wait for those loads.
+  constexpr int NCH = KT * HD / EPC / 256;  // 16-byte chunks of K (and of V) per thread per tile
+  uint4 kreg[NCH], vreg[NCH];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + i * 256;
       const int key = c / (HD / EPC), dc = c % (HD / EPC);
       const int kk = k0 + key;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
       if (kk < S) {
-        kv = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + D + h * HD + dc * EPC);
-        vv = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + 2 * D + h * HD + dc * EPC);
+        kreg[i] = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + D + h * HD + dc * EPC);
+        vreg[i] = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + 2 * D + h * HD + dc * EPC);
       }
-      *reinterpret_cast<uint4*>(Ks + key * LD + dc * EPC) = kv;
-      const T* ve = reinterpret_cast<const T*>(&vv);
+    }
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < S; k0 += KT) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous tile's Ks / Vt reads are done
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + i * 256;
+      const int key = c / (HD / EPC), dc = c % (HD / EPC);
+      *reinterpret_cast<uint4*>(Ks + key * LD + dc * EPC) = kreg[i];
+      const T* ve = reinterpret_cast<const T*>(&vreg[i]);
 #pragma unroll
       for (int e = 0; e < EPC; ++e) Vt[(dc * EPC + e) * VLD + key] = ve[e];
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (k0 + KT < S) fetch(k0 + KT);
 
     floatx4 sacc[4];
 #pragma unroll
@@ -144,7 +160,8 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv,
 #pragma unroll
       for (int dblk = 0; dblk < 4; ++dblk) o[dblk][r] *= alpha;
     }
-    __syncthreads();
+    // P is wave-private: its writes retired, the wave's own lanes read it back (no workgroup barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
