@@ -1140,7 +1140,7 @@ struct Knobs {
   };
   HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
   int n_halo_map = 0;
-  int xcd2d = 1;  // 2-D tile -> XCD rectangles (xcd_groups)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
+  int xcd2d = 2;  // 2-D tile -> XCD rectangles (xcd_groups); 2: not for split-K grids (plain order there)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
 
 Knobs read_knobs() {
@@ -1388,6 +1388,10 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
   xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, a.tiles_m, a.tiles / a.tiles_m, a.xg_m, a.xg_n);
+  if (pl.splits > 1 && knobs().xcd2d == 2) {  // split-K grids: the plain column-major order
+    a.xg_m = 1;
+    a.xg_n = std::min(8, a.tiles / a.tiles_m);
+  }
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
   // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
