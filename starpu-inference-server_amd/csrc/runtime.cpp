@@ -3,6 +3,8 @@
 // per-device pinned slot pools, parallel host staging, H2D on a copy stream
 // joined by events, batching strategies, and the client load generator.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <time.h>
 
 #include <algorithm>
@@ -217,6 +219,7 @@ struct SlotPool {
   std::mutex mu;
   std::condition_variable cv;
   hipStream_t copy_stream = nullptr;  // SPI_H2D_DEVICE_STREAM
+  hsa_agent_t gpu_agent{}, cpu_agent{};  // SPI_H2D_WORKER_SDMA
 
   int acquire() {
     std::unique_lock<std::mutex> lk(mu);
@@ -259,6 +262,7 @@ struct Worker {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // H2D stream (may be the pool's shared one)
   bool own_copy_stream = false;
+  hsa_signal_t h2d_signal{};  // SPI_H2D_WORKER_SDMA: completion of the task's SDMA copies
   std::deque<Task> inflight;
   std::deque<Job> fixed;  // jobs pinned to this worker (under the runtime mutex)
   std::thread thread;
@@ -268,6 +272,45 @@ struct Worker {
 };
 
 using QueueKey = std::pair<int64_t, uint64_t>;  // (-priority, submission sequence)
+
+// HIP device -> its HSA GPU agent (matched by PCI domain / bus / device) and the
+// first CPU agent, for SPI_H2D_WORKER_SDMA.  HIP has initialised HSA already.
+bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
+  int bus = 0, dev = 0, dom = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, device) != hipSuccess)
+    return false;
+  struct Find {
+    uint32_t bdf, dom;
+    hsa_agent_t gpu{}, cpu{};
+    bool g = false, c = false;
+  } f{(uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom};
+  if (hsa_init() != HSA_STATUS_SUCCESS) return false;  // reference-counted; HIP holds one too
+  hsa_iterate_agents(
+      [](hsa_agent_t a, void* u) {
+        Find& f = *static_cast<Find*>(u);
+        hsa_device_type_t t;
+        if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+        if (t == HSA_DEVICE_TYPE_CPU && !f.c) {
+          f.cpu = a;
+          f.c = true;
+        } else if (t == HSA_DEVICE_TYPE_GPU && !f.g) {
+          uint32_t bdf = 0, dom = 0;
+          hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+          hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+          if ((bdf & ~7u) == f.bdf && dom == f.dom) {
+            f.gpu = a;
+            f.g = true;
+          }
+        }
+        return HSA_STATUS_SUCCESS;
+      },
+      &f);
+  gpu = f.gpu;
+  cpu = f.cpu;
+  return f.g && f.c;
+}
 
 }  // namespace
 
@@ -391,7 +434,24 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
   const int64_t c2 = now_ns();
   // H2D into the slot's HBM buffers (StarPU's fetch of the R handles)
   hipStream_t h2d = w->copy_stream ? w->copy_stream : w->stream;
-  for (int i = 0; i < ni && t.status == SPI_OK; ++i)
+  if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
+    // SDMA engine copies (HIP's own hipMemcpyAsync takes a shader copy kernel for a
+    // share of these 4.8 MB copies, 256 workgroups for ~120 us each, competing with
+    // the forwards: DESIGN.md 5.1), waited here; the slot's HBM buffers are free (the
+    // slot was released after its last task's completion event)
+    const SlotPool& pl = *pools[w->pool];
+    hsa_signal_store_screlease(w->h2d_signal, ni);
+    for (int i = 0; i < ni; ++i)
+      if (hsa_amd_memory_async_copy(slot.d_in[i], pl.gpu_agent, slot.h_in[i], pl.cpu_agent,
+                                    (size_t)t.total * in_sample_bytes[i], 0, nullptr, w->h2d_signal) != HSA_STATUS_SUCCESS) {
+        t.status = SPI_ERR_DEVICE;
+        t.err = "SDMA H2D copy failed";
+        hsa_signal_subtract_screlease(w->h2d_signal, ni - i);
+        break;
+      }
+    hsa_signal_wait_scacquire(w->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+  }
+  for (int i = 0; i < ni && t.status == SPI_OK && cfg.h2d_mode != SPI_H2D_WORKER_SDMA; ++i)
     if (hipMemcpyAsync(slot.d_in[i], slot.h_in[i], (size_t)t.total * in_sample_bytes[i], hipMemcpyHostToDevice,
                        h2d) != hipSuccess) {
       t.status = SPI_ERR_DEVICE;
@@ -554,6 +614,7 @@ void spi_runtime::destroy_resources() {
   for (auto& w : workers) {
     (void)hipSetDevice(w->device);
     if (w->own_copy_stream && w->copy_stream) (void)hipStreamDestroy(w->copy_stream);
+    if (w->h2d_signal.handle) (void)hsa_signal_destroy(w->h2d_signal);
     if (w->stream) (void)hipStreamDestroy(w->stream);
   }
   for (auto& p : pools) {
@@ -655,7 +716,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   };
   if (!c || c->num_devices < 1 || c->num_devices > SPI_MAX_REPLICAS || c->max_batch < 1 || c->num_inputs < 1 ||
       c->num_inputs > SPI_MAX_INPUTS || c->num_outputs < 1 || c->num_outputs > SPI_MAX_OUTPUTS ||
-      c->h2d_mode < 0 || c->h2d_mode > SPI_H2D_AUTO || c->batching.kind < 0 ||
+      c->h2d_mode < 0 || c->h2d_mode > SPI_H2D_WORKER_SDMA || c->batching.kind < 0 ||
       c->batching.kind > SPI_BATCHING_ADAPTIVE)
     return fail("invalid runtime configuration");
   auto rt = std::make_unique<spi_runtime>();
@@ -727,6 +788,10 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     }
     if (ok && cfg.h2d_mode == SPI_H2D_DEVICE_STREAM)
       ok = hipStreamCreateWithFlags(&pool->copy_stream, hipStreamNonBlocking) == hipSuccess;
+    if (ok && cfg.h2d_mode == SPI_H2D_WORKER_SDMA && !find_hsa_agents(pool->device, pool->gpu_agent, pool->cpu_agent)) {
+      rt->pools.push_back(std::move(pool));
+      return cleanup_fail("no HSA agents for device " + std::to_string(c->device_ids[dv]));
+    }
     rt->pools.push_back(std::move(pool));
     if (!ok) return cleanup_fail("slot pool allocation failed on device " + std::to_string(c->device_ids[dv]));
     for (int k = 0; k < cfg.workers_per_device; ++k) {
@@ -741,6 +806,8 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       } else if (cfg.h2d_mode == SPI_H2D_WORKER_COPY) {
         wok = wok && hipStreamCreateWithFlags(&w->copy_stream, hipStreamNonBlocking) == hipSuccess;
         w->own_copy_stream = true;
+      } else if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
+        wok = wok && hsa_signal_create(0, 0, nullptr, &w->h2d_signal) == HSA_STATUS_SUCCESS;
       }
       rt->workers.push_back(std::move(w));
       if (!wok) return cleanup_fail("stream creation failed for worker " + std::to_string(wid - 1));

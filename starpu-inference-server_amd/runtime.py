@@ -17,7 +17,7 @@ from .codelet import ModelReplica, spi_dtype
 
 SPI_ERR_QUEUE_FULL = 8
 BATCHING = {"fixed": 0, "disabled": 1, "adaptive": 2}
-H2D_MODES = {"device_stream": 0, "worker_stream": 1, "worker_copy": 2, "auto": 3}
+H2D_MODES = {"device_stream": 0, "worker_stream": 1, "worker_copy": 2, "auto": 3, "worker_sdma": 4}
 
 
 class JobTiming(C.Structure):

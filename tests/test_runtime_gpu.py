@@ -17,10 +17,12 @@ def rtmod(spi, gpu):
     return importlib.import_module("starpu-inference-server_amd.runtime")
 
 
-def test_runtime_resnet_jobs_match_oracle(spi, zoo, rtmod):
+@pytest.mark.parametrize("h2d", ["auto", "worker_sdma"])
+def test_runtime_resnet_jobs_match_oracle(spi, zoo, rtmod, h2d):
     m = zoo.resnet18(image=64)
     rep = spi.ModelReplica(m, 0, "fp32", max_batch=4, image_size=64)
-    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=4, workers_per_device=3)
+    rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=4, workers_per_device=3,
+                       h2d_mode=h2d)
     rng = np.random.default_rng(0)
     jobs = []
     for rid in range(12):
@@ -41,11 +43,12 @@ def test_runtime_resnet_jobs_match_oracle(spi, zoo, rtmod):
     rt.close()
 
 
-def test_runtime_bert_two_inputs(spi, zoo, rtmod):
+@pytest.mark.parametrize("h2d", ["auto", "worker_sdma"])
+def test_runtime_bert_two_inputs(spi, zoo, rtmod, h2d):
     m = zoo.bert(layers=2)
     rep = spi.ModelReplica(m, 0, "fp16", max_batch=2, seq_len=32)
     rt = rtmod.Runtime([rep], [((32,), np.int64), ((32,), np.int64)], [(32 * 768, np.float32)], max_batch=2,
-                       workers_per_device=2)
+                       workers_per_device=2, h2d_mode=h2d)
     rng = np.random.default_rng(1)
     ids = rng.integers(0, 30522, (2, 32), dtype=np.int64)
     mask = np.ones((2, 32), dtype=np.int64)
