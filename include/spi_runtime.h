@@ -124,13 +124,16 @@ typedef void (*spi_job_done_fn)(void* user, int32_t request_id, int32_t status, 
 
 /* A device serves about four busy streams at once: with a fifth (four workers +
  * a copy stream, or five workers) one or two of them get a third of the others'
- * tasks.  SPI_H2D_AUTO keeps a device at <= 4 busy streams: a
- * shared copy stream for <= 3 workers, the H2D on the worker stream beyond. */
+ * tasks.  SPI_H2D_AUTO takes the SDMA engines directly (no stream,
+ * and no H2D turned into a shader copy kernel beside the forwards); without HSA
+ * agents it keeps a device at <= 4 busy streams: a shared copy stream for <= 3
+ * workers, the H2D on the worker stream beyond. */
 enum spi_h2d_mode {
   SPI_H2D_DEVICE_STREAM = 0, /* one copy stream per device, event-joined */
   SPI_H2D_WORKER_STREAM = 1, /* H2D on the worker's own stream */
   SPI_H2D_WORKER_COPY = 2,   /* one copy stream per worker, event-joined */
-  SPI_H2D_AUTO = 3,          /* default: DEVICE_STREAM for <= 3 workers per device, else WORKER_STREAM */
+  SPI_H2D_AUTO = 3,          /* default: WORKER_SDMA; if the HSA agents cannot be resolved, DEVICE_STREAM
+                                for <= 3 workers per device, else WORKER_STREAM */
   SPI_H2D_WORKER_SDMA = 4    /* H2D on an SDMA engine (hsa_amd_memory_async_copy), waited by the worker
                                 thread before the codelet is enqueued: no stream, no shader copy kernel */
 };

@@ -20,17 +20,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--requests", type=int, default=4000)
     ap.add_argument("--modes", default="auto,worker_sdma")
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--precision", default="fp16m")
     args = ap.parse_args()
     spi = importlib.import_module("starpu-inference-server_amd")
     zoo = importlib.import_module("starpu-inference-server_amd.zoo")
     rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
     import bench
-    rep = spi.ModelReplica(zoo.build("resnet18", seed=0), 0, "fp16m", max_batch=8, graphs=True)
+    rep = spi.ModelReplica(zoo.build(args.model, seed=0), 0, args.precision, max_batch=args.batch, graphs=True)
     for r in range(args.rounds):
-        for mode in args.modes.split(","):
+        for spec in args.modes.split(","):
+            mode, _, wait = spec.partition(":")  # "worker_sdma:blocked" sleeps on the copy signal
+            os.environ["SPI_H2D_SDMA_WAIT"] = wait
             for inflight in (32, 16):
-                out = bench.runtime_e2e(rtmod, rep, "resnet18", 8, args.requests, inflight, h2d_mode=mode)
-                print(json.dumps({"round": r, "h2d_mode": mode, "inflight": inflight, **out}), flush=True)
+                out = bench.runtime_e2e(rtmod, rep, args.model, args.batch, args.requests, inflight, h2d_mode=mode)
+                print(json.dumps({"round": r, "h2d_mode": spec, "inflight": inflight, **out}), flush=True)
 
 
 if __name__ == "__main__":
