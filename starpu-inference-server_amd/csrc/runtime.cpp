@@ -727,11 +727,30 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   rt->cfg = *c;
   spi_runtime_config& cfg = rt->cfg;
   if (cfg.workers_per_device <= 0) cfg.workers_per_device = 4;
+  if (cfg.pipeline_depth <= 0) cfg.pipeline_depth = 2;
+  if (cfg.copy_threads <= 0) cfg.copy_threads = 4;
+  if (cfg.slots_per_device <= 0) cfg.slots_per_device = std::max(2, cfg.workers_per_device * cfg.pipeline_depth);
+  if (cfg.batching.batch_limit <= 0 || cfg.batching.batch_limit > cfg.max_batch) cfg.batching.batch_limit = cfg.max_batch;
+  for (int i = 0; i < c->num_inputs; ++i) {
+    size_t n = spi_dtype_size(c->input_types[i]);
+    if (!n || c->input_ndims[i] < 0 || c->input_ndims[i] >= SPI_MAX_DIMS) return fail("invalid input spec");
+    for (int d = 0; d < c->input_ndims[i]; ++d) n *= (size_t)c->input_dims[i][d];
+    rt->in_sample_bytes.push_back(n);
+  }
+  for (int i = 0; i < c->num_outputs; ++i) {
+    const size_t es = spi_dtype_size(c->output_types[i]);
+    if (!es || c->output_elems[i] <= 0) return fail("invalid output spec");
+    rt->out_sample_bytes.push_back(es * (size_t)c->output_elems[i]);
+  }
   if (cfg.h2d_mode == SPI_H2D_AUTO) {
-    // SDMA-engine copies when every device's HSA agents resolve (ResNet-18 bs8 e2e 64-68k ->
-    // 81-85k inf/s); else the stream copies: a shared copy stream for <= 3
-    // workers, the worker streams beyond (four busy streams per device)
-    bool sdma = true;
+    // SDMA-engine copies for task inputs up to 8 MiB when every device's HSA agents
+    // resolve (ResNet-18 bs8, 4.8 MB: e2e 64-68k -> 81-85k inf/s; ResNet-152 bs32,
+    // 19.3 MB: 10.5k -> 9.5k, so larger inputs keep the stream copies -- DESIGN.md 4);
+    // the stream copies: a shared copy stream for <= 3 workers, the worker streams
+    // beyond (four busy streams per device)
+    size_t task_in = 0;
+    for (size_t b : rt->in_sample_bytes) task_in += b * (size_t)cfg.max_batch;
+    bool sdma = task_in <= (size_t(8) << 20);
     for (int dv = 0; dv < c->num_devices && sdma; ++dv) {
       hsa_agent_t g{}, h{};
       sdma = find_hsa_agents(c->device_ids[dv], g, h);
@@ -739,10 +758,6 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     cfg.h2d_mode = sdma ? SPI_H2D_WORKER_SDMA
                         : cfg.workers_per_device <= 3 ? SPI_H2D_DEVICE_STREAM : SPI_H2D_WORKER_STREAM;
   }
-  if (cfg.pipeline_depth <= 0) cfg.pipeline_depth = 2;
-  if (cfg.copy_threads <= 0) cfg.copy_threads = 4;
-  if (cfg.slots_per_device <= 0) cfg.slots_per_device = std::max(2, cfg.workers_per_device * cfg.pipeline_depth);
-  if (cfg.batching.batch_limit <= 0 || cfg.batching.batch_limit > cfg.max_batch) cfg.batching.batch_limit = cfg.max_batch;
   {
     // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4)
     // round-robin; worker streams sharing a queue run serially.
@@ -755,17 +770,6 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
                    "spi_runtime: GPU_MAX_HW_QUEUES=%d < %d streams + 1; streams will share hardware queues and "
                    "serialize (set it before the first HIP call)\n",
                    queues, need);
-  }
-  for (int i = 0; i < c->num_inputs; ++i) {
-    size_t n = spi_dtype_size(c->input_types[i]);
-    if (!n || c->input_ndims[i] < 0 || c->input_ndims[i] >= SPI_MAX_DIMS) return fail("invalid input spec");
-    for (int d = 0; d < c->input_ndims[i]; ++d) n *= (size_t)c->input_dims[i][d];
-    rt->in_sample_bytes.push_back(n);
-  }
-  for (int i = 0; i < c->num_outputs; ++i) {
-    const size_t es = spi_dtype_size(c->output_types[i]);
-    if (!es || c->output_elems[i] <= 0) return fail("invalid output spec");
-    rt->out_sample_bytes.push_back(es * (size_t)c->output_elems[i]);
   }
   for (int dv = 0; dv < c->num_devices; ++dv)
     if (!c->models[dv]) return fail("missing replica for device " + std::to_string(c->device_ids[dv]));

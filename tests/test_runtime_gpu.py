@@ -17,7 +17,7 @@ def rtmod(spi, gpu):
     return importlib.import_module("starpu-inference-server_amd.runtime")
 
 
-@pytest.mark.parametrize("h2d", ["auto", "worker_sdma"])
+@pytest.mark.parametrize("h2d", ["worker_stream", "device_stream", "worker_sdma"])
 def test_runtime_resnet_jobs_match_oracle(spi, zoo, rtmod, h2d):
     m = zoo.resnet18(image=64)
     rep = spi.ModelReplica(m, 0, "fp32", max_batch=4, image_size=64)
@@ -43,7 +43,7 @@ def test_runtime_resnet_jobs_match_oracle(spi, zoo, rtmod, h2d):
     rt.close()
 
 
-@pytest.mark.parametrize("h2d", ["auto", "worker_sdma"])
+@pytest.mark.parametrize("h2d", ["worker_stream", "device_stream", "worker_sdma"])
 def test_runtime_bert_two_inputs(spi, zoo, rtmod, h2d):
     m = zoo.bert(layers=2)
     rep = spi.ModelReplica(m, 0, "fp16", max_batch=2, seq_len=32)
