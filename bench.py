@@ -474,7 +474,7 @@ def main():
         e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=8 * args.workers,
                           workers=args.workers)
         e2e["fraction_of_device_resident"] = round(e2e["value"] / value, 4)
-        e2e["pipeline"] = ("4 workers x depth 2, H2D by an SDMA engine per task (SPI_H2D_AUTO = WORKER_SDMA for inputs <= 8 MiB: "
+        e2e["pipeline"] = ("4 workers x depth 2, H2D by an SDMA engine per task (SPI_H2D_AUTO = WORKER_SDMA for >= 64 KiB of input per GFLOP: "
                            "hsa_amd_memory_async_copy waited by the worker thread, no copy stream or shader copy "
                            "kernel), pinned slot pool of 8, 4 host copy threads")
         result["e2e"] = e2e

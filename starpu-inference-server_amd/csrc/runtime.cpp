@@ -743,14 +743,16 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     rt->out_sample_bytes.push_back(es * (size_t)c->output_elems[i]);
   }
   if (cfg.h2d_mode == SPI_H2D_AUTO) {
-    // SDMA-engine copies for task inputs up to 8 MiB when every device's HSA agents
-    // resolve (ResNet-18 bs8, 4.8 MB: e2e 64-68k -> 81-85k inf/s; ResNet-152 bs32,
-    // 19.3 MB: 10.5k -> 9.5k, so larger inputs keep the stream copies -- DESIGN.md 4);
-    // the stream copies: a shared copy stream for <= 3 workers, the worker streams
-    // beyond (four busy streams per device)
+    // SDMA-engine copies when the task's input would keep the PCIe link busy: at least
+    // 64 KiB per GFLOP of the forward (at the ~350 TFLOP/s the ResNet-18 headline sustains
+    // a GFLOP is ~3 us, 64 KiB over the 51 GB/s link ~1.3 us) -- ResNet-18 (166 KiB/GFLOP):
+    // e2e 64-68k -> 81-85k inf/s; ResNet-152 (26), ViT-L (5), BERT (0.1) are compute-bound
+    // and measured 5-10 % better on the stream copies.  Those: a shared copy
+    // stream for <= 3 workers, the worker streams beyond (four busy streams per device)
     size_t task_in = 0;
     for (size_t b : rt->in_sample_bytes) task_in += b * (size_t)cfg.max_batch;
-    bool sdma = task_in <= (size_t(8) << 20);
+    const double gflop = c->models[0] ? spi_model_flops(c->models[0], cfg.max_batch) * 1e-9 : 0.0;
+    bool sdma = gflop > 0.0 && (double)task_in / gflop >= 64.0 * 1024.0;
     for (int dv = 0; dv < c->num_devices && sdma; ++dv) {
       hsa_agent_t g{}, h{};
       sdma = find_hsa_agents(c->device_ids[dv], g, h);
