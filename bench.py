@@ -36,6 +36,8 @@ import glob
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -274,8 +276,12 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
     else:
         in_specs = [((3, 224, 224), np.float32)]
     out_elems = int(np.prod(out_shape[1:]))
+    # every task is max_batch when requests are max_batch and nothing merges them: warm that size only
+    if rb == batch and "warmup_batches" not in kw:
+        kw["warmup_batches"] = -1
     rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers,
                        **kw)
+    h2d = rt.h2d_mode
     r = rt.loadgen(host_inputs, requests=requests, inflight=inflight, warmup=4 * workers * 2, schedule=schedule)
     target = rt.batch_target
     rt.close()
@@ -284,7 +290,7 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
            "requests": r["completed"], "request_batch": rb, "max_batch": batch, "inflight": inflight,
            "workers": workers, "mean_task_batch": round(r["mean_task_batch"], 2),
            "p50_queue_ms": round(r["p50_queue_ms"], 4), "failed": r["failed"], "rejected": r["rejected"],
-           "seconds": round(r["seconds"], 3)}
+           "seconds": round(r["seconds"], 3), "h2d_mode": h2d}
     if r["error"]:
         out["first_error"] = r["error"]
     if kw.get("batching") is not None:
@@ -292,7 +298,31 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
     return out
 
 
+def aggregate_e2e(local: dict, world: int, dist) -> dict:
+    """Whole-job serving figures over the ranks (one runtime per GPU, each rank's loop started
+    behind a barrier): inferences of all ranks / the longest rank's (last response - first
+    request); p50/p95/p99 the worst rank's (per-rank values listed)."""
+    if world <= 1:
+        return local
+    per = [None] * world
+    dist.all_gather_object(per, local)
+    inf = sum(p["requests"] * p["request_batch"] for p in per)
+    sec = max(p["seconds"] for p in per)
+    out = dict(local)
+    out.update({"value": round(inf / sec, 2) if sec > 0 else 0.0, "requests": sum(p["requests"] for p in per),
+                "seconds": sec, "failed": sum(p["failed"] for p in per), "rejected": sum(p["rejected"] for p in per),
+                "p50_latency_ms": max(p["p50_latency_ms"] for p in per),
+                "p95_latency_ms": max(p["p95_latency_ms"] for p in per),
+                "p99_latency_ms": max(p["p99_latency_ms"] for p in per),
+                "per_rank": [{k: p[k] for k in ("value", "p50_latency_ms", "p99_latency_ms")} for p in per],
+                "aggregation": "sum of inferences over ranks / longest rank window; worst rank's percentiles"})
+    return out
+
+
 def host_cores():
+    """The host as this process sees it.  `threads_used`: the CPU share of the job -- the GPU box
+    allots OMP_NUM_THREADS (16) CPUs per GPU and asks jobs to stay inside it -- else every
+    affinity CPU."""
     nodes = glob.glob("/sys/devices/system/node/node[0-9]*")
     try:
         affinity = len(os.sched_getaffinity(0))
@@ -300,13 +330,17 @@ def host_cores():
         affinity = os.cpu_count()
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
     return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "numa_nodes": max(1, len(nodes)),
-            "threads_used": min(share, affinity)}
+            "threads_used": min(share, affinity),
+            "share_rule": "OMP_NUM_THREADS (the box's CPU share per GPU)" if share < affinity else "affinity CPUs"}
 
 
 def cpu_baseline(model, name, batch, seconds):
     """The C++ LibTorch CPU codelet (spi_cpu_inference_func + spi_torch_cpu_forward) on a TorchScript
-    export of the same model: layout (i) one worker with all the host threads as intra-op threads
-    (group_cpu_by_numa, starpu_setup.cpp:299-385), layout (ii) one worker per NUMA node."""
+    export of the same model, in the reference's CPU-worker layouts (starpu_setup.cpp:291-386):
+    (i) one worker with every thread of the share as intra-op threads, (ii) one worker per NUMA
+    node (group_cpu_by_numa), (iii) the default, one StarPU CPU worker per core with one intra-op
+    thread each.  The per-core rate of (iii) times the host's affinity CPUs is reported as an
+    extrapolation (never measured beyond the share)."""
     import torch
 
     lt = importlib.import_module("starpu-inference-server_amd.libtorch")
@@ -320,44 +354,85 @@ def cpu_baseline(model, name, batch, seconds):
     rng = np.random.default_rng(0)
     x8 = rng.random((batch, 3, 224, 224), dtype=np.float32)
     x1 = x8[:1].copy()
-    # warm-up, then ~seconds of CPU work per configuration
-    ts.bench([x1], [4000], workers=1, threads=n, seconds=0.5)
-    main = ts.bench([x8], [batch * 4000], workers=1, threads=n, seconds=seconds)
-    c1 = ts.bench([x1], [4000], workers=1, threads=n, seconds=seconds / 2)
     per = max(1, n // numa)
-    c1_numa = ts.bench([x1], [4000], workers=numa, threads=per, seconds=seconds / 2)
+    layouts = {"i_one_worker_all_threads": (1, n), "ii_worker_per_numa_node": (numa, per),
+               "iii_worker_per_core": (n, 1)}
+    ts.bench([x1], [4000], workers=1, threads=n, seconds=0.5)  # warm-up
+    main = {}
+    for key in ("i_one_worker_all_threads", "iii_worker_per_core"):
+        w, t = layouts[key]
+        r = ts.bench([x8], [batch * 4000], workers=w, threads=t, seconds=seconds / 3)
+        main[key] = {"value": round(r["inferences_per_s"], 3), "p50_ms": round(r["p50_ms"], 3), "workers": w,
+                     "threads_per_worker": t, "tasks": r["tasks"]}
+    c1 = {}
+    if name == "resnet18":
+        for key, (w, t) in layouts.items():
+            r = ts.bench([x1], [4000], workers=w, threads=t, seconds=seconds / 3)
+            c1[key] = {"value": round(r["inferences_per_s"], 3), "unit": "inferences/s",
+                       "p50_ms": round(r["p50_ms"], 3), "workers": w, "threads_per_worker": t, "tasks": r["tasks"]}
     ts.close()
-    return {
-        "value": round(main["inferences_per_s"], 3), "unit": "inferences/s", "cores": n, "kind": "port",
-        "sample": f"{main['tasks']} CPU-codelet tasks ({name} bs{batch} fp32, TorchScript, libspi_torch.so: "
-                  f"InferenceMode forward + copy_output_to_buffer behind spi_cpu_inference_func), "
-                  f"{main['seconds']:.1f} s, 1 worker x {n} intra-op threads",
-        "p50_ms": round(main["p50_ms"], 3), "host": cores,
-        "c1_resnet18_bs1_fp32": {
-            "layout_i_one_worker_all_threads": {"value": round(c1["inferences_per_s"], 3), "unit": "inferences/s",
-                                                "p50_ms": round(c1["p50_ms"], 3), "workers": 1, "threads": n,
-                                                "tasks": c1["tasks"]},
-            "layout_ii_worker_per_numa_node": {"value": round(c1_numa["inferences_per_s"], 3),
-                                               "unit": "inferences/s", "p50_ms": round(c1_numa["p50_ms"], 3),
-                                               "workers": numa, "threads_per_worker": per,
-                                               "tasks": c1_numa["tasks"]}} if name == "resnet18" else None,
+    best = max(main, key=lambda k: main[k]["value"])
+    out = {
+        "value": main[best]["value"], "unit": "inferences/s", "cores": n, "kind": "port",
+        "sample": f"CPU-codelet tasks ({name} bs{batch} fp32, TorchScript, libspi_torch.so: InferenceMode forward + "
+                  f"copy_output_to_buffer behind spi_cpu_inference_func), ~{seconds / 3:.1f} s per layout; value = "
+                  f"best layout ({best})",
+        "p50_ms": main[best]["p50_ms"], "host": cores, "layouts_bs%d" % batch: main,
     }
+    if c1:
+        per_core = c1["iii_worker_per_core"]["value"] / max(1, n)
+        c1["extrapolated_full_host_per_core_layout"] = {
+            "value": round(per_core * cores["affinity_cpus"], 1), "unit": "inferences/s",
+            "basis": f"layout (iii) per-core rate x {cores['affinity_cpus']} affinity CPUs (not measured: the box "
+                     f"allots {n} CPUs to this job)"}
+        out["c1_resnet18_bs1_fp32"] = c1
+    return out
 
 
-def config_line(spi, zoo, name, batch, precision, workers, streams, steps, dev, seq=128):
-    """Device-resident inf/s, loaded p50 task latency and roofline for one BASELINE config."""
+def config_line(spi, zoo, rtmod, name, batch, precision, workers, streams, steps, dev, rank, world, dist, seq=128,
+                e2e_requests=400):
+    """Device-resident inf/s (all ranks), loaded p50 task latency and roofline (rank 0), and the
+    PCIe-inclusive e2e run (all ranks, aggregated) for one BASELINE config."""
     model = zoo.build(name, seed=0)
     rep = spi.ModelReplica(model, dev, precision, max_batch=batch, seq_len=seq if name.startswith("bert") else 0,
                            graphs=True)
-    h = Harness(spi, rep, name, dev, batch, workers, np.random.default_rng(3), streams)
-    el = h.throughput(steps, 2, 1)
+    h = Harness(spi, rep, name, dev, batch, workers, np.random.default_rng(3 + rank), streams)
+    el = h.throughput(steps, 2, 1, world, dist)
     lat = h.loaded_latency(10)
-    out = {"value": round(workers * batch * steps / el, 2), "unit": "sequences/s" if name.startswith("bert") else
-           "inferences/s", "dtype": precision, "batch": batch,
-           "p50_task_latency_ms": round(percentile(lat, 50), 4),
-           "gflop_per_inference": round(rep.flops(1) / 1e9, 3), "roofline": roofline(h, precision, name)}
-    out["model_tflops"] = round(rep.flops(1) * out["value"] / 1e12, 2)
-    return out, rep, model
+    out = {"value": round(world * workers * batch * steps / el, 2),
+           "unit": "sequences/s" if name.startswith("bert") else "inferences/s", "dtype": precision, "batch": batch,
+           "n_gpus": world, "p50_task_latency_ms": round(percentile(lat, 50), 4),
+           "gflop_per_inference": round(rep.flops(1) / 1e9, 3)}
+    if rank == 0:
+        out["roofline"] = roofline(h, precision, name)
+    out["model_tflops_per_gpu"] = round(rep.flops(1) * out["value"] / world / 1e12, 2)
+    if world > 1:
+        dist.barrier()
+    out["e2e"] = aggregate_e2e(runtime_e2e(rtmod, rep, name, batch, e2e_requests, inflight=4 * workers,
+                                           workers=workers), world, dist)
+    del rep, model, h
+    return out
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE set, as torch.distributed.run would) before this process touches any
+    GPU, pass rank 0's JSON line through, and exit with the worst return code."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
 
 
 def main():
@@ -374,15 +449,26 @@ def main():
     ap.add_argument("--repeats", type=int, default=5,
                     help="re-time the same K-step region this many times after `value` (value_repeats)")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline budget per layout (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=9.0, help="CPU baseline budget over its layouts (0 = skip)")
     ap.add_argument("--e2e-requests", type=int, default=4000)
-    ap.add_argument("--extras", type=int, default=1, help="single-GPU extra measurements (0 = skip)")
+    ap.add_argument("--extras", type=int, default=1, help="extra measurements (0 = skip)")
+    ap.add_argument("--ci-schedule", type=int, default=1,
+                    help="the reference's CI perf workload (ResNet-152, bs1 requests, adaptive batching to 16, "
+                         "ci_perf_resnet.csv at its real intervals: ~14 s)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant op's back-to-back launches (the rocprofv3 roofline command)")
     ap.add_argument("--roofline-op", default="", help="op name for --roofline-only (default: chosen under load)")
     ap.add_argument("--roofline-reps", type=int, default=200)
+    ap.add_argument("--control-plane-only", action="store_true",
+                    help="test hook (tests/test_host.py): run the multi-rank control path -- rank spawn, gloo "
+                         "rendezvous, barrier + max-over-ranks timing, e2e aggregation, the JSON line -- around "
+                         "a host-side stand-in for the GPU work")
     args = ap.parse_args()
     args.precision = args.precision or DEFAULT_PRECISION[args.model]
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
     # One HIP hardware queue per stream: HIP maps streams onto GPU_MAX_HW_QUEUES queues
     # round-robin (default 4, shared with torch's own streams), and streams that share a queue
     # run serially -- 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues.  Room for the
@@ -398,13 +484,16 @@ def main():
     import torch
     import torch.distributed as dist
 
-    spi = importlib.import_module("starpu-inference-server_amd")
-    zoo = importlib.import_module("starpu-inference-server_amd.zoo")
-    rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
-
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.control_plane_only:
+        control_plane_only(args, rank, world, dist)
+        return
+
+    spi = importlib.import_module("starpu-inference-server_amd")
+    zoo = importlib.import_module("starpu-inference-server_amd.zoo")
+    rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
     # SPI_BENCH_SHARE_DEVICE=1: every rank on device 0 (multi-rank rehearsal on a 1-GPU box only).
     dev = 0 if os.environ.get("SPI_BENCH_SHARE_DEVICE") == "1" else local_rank
     torch.cuda.set_device(dev)
@@ -454,7 +543,9 @@ def main():
                                "fp16m": "fp16 MFMA operands + fp16 activations, fp32 accumulate; stem / downsample / "
                                         "FC on split-fp16 weights (normalised max error 0.5-0.6e-3 at this config)",
                                "fp16": "fp16 MFMA operands, fp32 accumulate", "fp32": "fp32 MFMA"}[args.precision],
-            "inputs": "resident in HBM (device-resident codelet rate; the PCIe-inclusive serving rate is `e2e`)",
+            "inputs": "resident in HBM when the timed region starts (the bench contract's `value`); the "
+                      "PCIe-inclusive serving rate -- submit -> outputs in host memory, SURVEY 8(d) -- is `e2e`, "
+                      "measured at every N",
             "graphs": bool(args.graphs),
             "hip_hw_queues": queues,
             "parallelism": f"replicas x{world} (request sharding, no collective)",
@@ -467,78 +558,43 @@ def main():
         result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
         result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
         result["roofline"] = roofline(h, args.precision, args.model, args.roofline_reps)
-    if rank == 0 and world == 1:
-        # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
-        # closed loop, 8 requests in flight per worker (the H2D link -- 51 GB/s measured, 85k inf/s of
-        # fp32 NCHW bs8 input -- and the compute pipeline both stay busy); and half that load
-        e2e = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=8 * args.workers,
-                          workers=args.workers)
-        e2e["fraction_of_device_resident"] = round(e2e["value"] / value, 4)
-        e2e["pipeline"] = ("4 workers x depth 2, H2D by an SDMA engine per task (SPI_H2D_AUTO = WORKER_SDMA for >= 64 KiB of input per GFLOP: "
-                           "hsa_amd_memory_async_copy waited by the worker thread, no copy stream or shader copy "
-                           "kernel), pinned slot pool of 8, 4 host copy threads")
-        result["e2e"] = e2e
-        half = runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests, inflight=4 * args.workers,
-                           workers=args.workers)
-        result["e2e_half_load"] = {k: half[k] for k in ("value", "unit", "p50_latency_ms", "p95_latency_ms",
-                                                        "p99_latency_ms", "requests", "inflight")}
-        e2e1 = h.serial_e2e(40)
-        result["p50_serial_e2e_latency_ms"] = round(percentile(e2e1, 50), 4)
+    # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
+    # closed loop on every rank's GPU, 8 requests in flight per worker (the H2D link -- 51 GB/s
+    # measured, 85k inf/s of fp32 NCHW bs8 input -- and the compute pipeline both stay busy), and
+    # half that load
+    if world > 1:
+        dist.barrier()
+    e2e = aggregate_e2e(runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests,
+                                    inflight=8 * args.workers, workers=args.workers), world, dist)
+    e2e["fraction_of_device_resident"] = round(e2e["value"] / value, 4)
+    e2e["pipeline"] = (f"{args.workers} workers x depth 2 per GPU, H2D {e2e['h2d_mode']} (SPI_H2D_AUTO), pinned slot "
+                       f"pool of {2 * args.workers}, 4 host copy threads, every batch size warmed up")
+    result["e2e"] = e2e
+    if world > 1:
+        dist.barrier()
+    half = aggregate_e2e(runtime_e2e(rtmod, replica, args.model, args.batch, args.e2e_requests,
+                                     inflight=4 * args.workers, workers=args.workers), world, dist)
+    result["e2e_half_load"] = {k: half[k] for k in ("value", "unit", "p50_latency_ms", "p95_latency_ms",
+                                                    "p99_latency_ms", "requests", "inflight")}
+    e2e1 = h.serial_e2e(40)
+    result["p50_serial_e2e_latency_ms"] = round(percentile(e2e1, 50), 4)
 
     if rank == 0 and args.cpu_seconds > 0 and args.model == "resnet18":
         result["cpu_baseline"] = cpu_baseline(model, args.model, args.batch, args.cpu_seconds)
 
-    if rank == 0 and world == 1 and args.extras and args.model == "resnet18":
+    if args.extras and args.model == "resnet18":
         extras = {}
-        # the same workload in the other modes: fp16x3 (fp32-grade, ~2e-6) and plain fp16
-        # operands everywhere (1.8e-3 .. 2.0e-3: misses the 1e-3 bar, never the C2 figure)
-        for prec in [p for p in ("fp16x3", "fp16") if p != args.precision]:
-            rp = spi.ModelReplica(model, dev, prec, max_batch=args.batch, graphs=True)
-            hp = Harness(spi, rp, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
-            el = hp.throughput(args.steps, 2, args.tasks_per_step)
-            extras[f"resnet18_bs8_{prec}"] = {
-                "value": round(per_step * args.steps / el, 2), "unit": "inferences/s",
-                "p50_task_latency_ms": round(percentile(hp.loaded_latency(10), 50), 4),
-                "parity": "fp32-grade (1.6e-6 .. 3.2e-6)" if prec == "fp16x3" else
-                          "1.8e-3 .. 2.0e-3 normalised max error: misses the 1e-3 bar, not a C2 result"}
-            del rp, hp
-        # ResNet-18 bs=1 (the metric names it): device-resident tasks, and bs1 requests served
-        r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
-        h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2), h.streams)
-        el = h1.throughput(args.steps, 2, args.tasks_per_step)
-        lat1 = h1.loaded_latency(20)
-        ser1 = h1.serial_e2e(40)
-        extras["resnet18_bs1_tasks"] = {
-            "value": round(args.workers * args.tasks_per_step * args.steps / el, 2), "unit": "inferences/s",
-            "p50_task_latency_ms": round(percentile(lat1, 50), 4),
-            "p50_serial_e2e_latency_ms": round(percentile(ser1, 50), 4), "dtype": args.precision}
-        del r1, h1
-        # bs1 client requests batched server-side into codelet calls of <= 8: closed loop, and the
-        # bursty open-loop schedule shaped like ci/perf/ci_perf_resnet.csv (delta_us x repeat, time
-        # scaled by 1/10 for this GPU), fixed coalescer vs adaptive strategy
-        extras["resnet18_bs1_requests_closed_loop_adaptive"] = runtime_e2e(
-            rtmod, replica, "resnet18", args.batch, 6000, inflight=64, req_batch=1,
-            batching=rtmod.batching_config("adaptive", 1, args.batch, coalesce_timeout_us=200, congestion=True,
-                                           tick_us=500, entry_horizon_us=3000, exit_horizon_us=7000))
-        sched = [(170, 3000), (30, 300), (300, 3000)]
-        for label, kw in [("fixed", dict(coalesce_max_jobs=args.batch, coalesce_delay_us=500)),
-                          ("adaptive", dict(batching=rtmod.batching_config(
-                              "adaptive", 1, args.batch, coalesce_timeout_us=500, congestion=True, tick_us=500,
-                              entry_horizon_us=3000, exit_horizon_us=7000)))]:
-            extras[f"resnet18_bs1_requests_bursty_schedule_{label}"] = runtime_e2e(
-                rtmod, replica, "resnet18", args.batch, 0, inflight=256, req_batch=1, max_queue=256,
-                schedule=sched, **kw)
-            extras[f"resnet18_bs1_requests_bursty_schedule_{label}"]["schedule_delta_us_repeat"] = sched
-        # C3 BERT-base seq128 bs8 fp16; C4 ResNet-152 bs32 fp16x3; C5 ViT-L/16 bs16 fp16 (single GPU)
+        if world == 1:
+            extras.update(single_gpu_extras(spi, zoo, rtmod, args, model, replica, h, dev, per_step))
+        # C3 BERT-base seq128 bs8 fp16; C4 ResNet-152 bs32 fp16x3; C5 ViT-L/16 bs16 fp16 -- at every N
         for key, name, b, prec in [("c3_bert_base_seq128_bs8_fp16", "bert_base", 8, "fp16"),
                                    ("c4_resnet152_bs32_fp16x3", "resnet152", 32, "fp16x3"),
                                    ("c5_vit_l_16_bs16_fp16", "vit_l_16", 16, "fp16")]:
-            line, rep, mdl = config_line(spi, zoo, name, b, prec, args.workers, h.streams, max(10, args.steps // 2),
-                                         dev)
-            line["e2e"] = runtime_e2e(rtmod, rep, name, b, 400 if name != "bert_base" else 1000,
-                                      inflight=4 * args.workers, workers=args.workers)
-            extras[key] = line
-            del rep, mdl
+            if world > 1:
+                dist.barrier()
+            extras[key] = config_line(spi, zoo, rtmod, name, b, prec, args.workers, h.streams,
+                                      max(10, args.steps // 2), dev, rank, world, dist,
+                                      e2e_requests=400 if name != "bert_base" else 1000)
         result["extras"] = extras
 
     if world > 1:
@@ -546,6 +602,99 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def control_plane_only(args, rank, world, dist):
+    """The multi-rank control path with the GPU work replaced by a sleep of (rank + 1) ms per
+    step: value must come from the slowest rank's window, e2e from the aggregation."""
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(args.steps * (rank + 1) * 1e-3)
+    elapsed = reduce_max_elapsed(time.perf_counter() - t0, world)
+    if world > 1:
+        dist.barrier()
+    per_step = args.workers * args.tasks_per_step * args.batch
+    local = {"value": 1000.0 * (rank + 1), "unit": "inferences/s", "requests": 100, "request_batch": args.batch,
+             "seconds": 0.1 * (rank + 1), "failed": 0, "rejected": 0, "p50_latency_ms": 1.0 + rank,
+             "p95_latency_ms": 2.0 + rank, "p99_latency_ms": 3.0 + rank}
+    e2e = aggregate_e2e(local, world, dist)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": BASELINE_METRIC, "value": round(world * per_step * args.steps / elapsed, 2),
+                          "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+                          "e2e": e2e, "control_plane_only": True}), flush=True)
+
+
+def single_gpu_extras(spi, zoo, rtmod, args, model, replica, h, dev, per_step):
+    """Rank 0 at N = 1: the headline workload in the other precision modes, ResNet-18 bs1, bs1
+    requests batched by the runtime, and the reference's own CI perf workload."""
+    extras = {}
+    # the same workload in the other modes: fp16x3 (fp32-grade, ~2e-6) and plain fp16
+    # operands everywhere (1.8e-3 .. 2.0e-3: misses the 1e-3 bar, never the C2 figure)
+    for prec in [p for p in ("fp16x3", "fp16") if p != args.precision]:
+        rp = spi.ModelReplica(model, dev, prec, max_batch=args.batch, graphs=True)
+        hp = Harness(spi, rp, "resnet18", dev, args.batch, args.workers, np.random.default_rng(1), h.streams)
+        el = hp.throughput(args.steps, 2, args.tasks_per_step)
+        extras[f"resnet18_bs8_{prec}"] = {
+            "value": round(per_step * args.steps / el, 2), "unit": "inferences/s",
+            "p50_task_latency_ms": round(percentile(hp.loaded_latency(10), 50), 4),
+            "parity": "fp32-grade (1.6e-6 .. 3.2e-6)" if prec == "fp16x3" else
+                      "1.8e-3 .. 2.0e-3 normalised max error: misses the 1e-3 bar, not a C2 result"}
+        del rp, hp
+    # ResNet-18 bs=1 (the metric names it): device-resident tasks, and bs1 requests served
+    r1 = spi.ModelReplica(model, dev, args.precision, max_batch=1, graphs=True)
+    h1 = Harness(spi, r1, "resnet18", dev, 1, args.workers, np.random.default_rng(2), h.streams)
+    el = h1.throughput(args.steps, 2, args.tasks_per_step)
+    lat1 = h1.loaded_latency(20)
+    ser1 = h1.serial_e2e(40)
+    extras["resnet18_bs1_tasks"] = {
+        "value": round(args.workers * args.tasks_per_step * args.steps / el, 2), "unit": "inferences/s",
+        "p50_task_latency_ms": round(percentile(lat1, 50), 4),
+        "p50_serial_e2e_latency_ms": round(percentile(ser1, 50), 4), "dtype": args.precision}
+    del r1, h1
+    # bs1 client requests batched server-side into codelet calls of <= 8: closed loop, and the
+    # bursty open-loop schedule shaped like ci/perf/ci_perf_resnet.csv (delta_us x repeat, time
+    # scaled by 1/10 for ResNet-18), fixed coalescer vs adaptive strategy
+    extras["resnet18_bs1_requests_closed_loop_adaptive"] = runtime_e2e(
+        rtmod, replica, "resnet18", args.batch, 6000, inflight=64, req_batch=1,
+        batching=rtmod.batching_config("adaptive", 1, args.batch, coalesce_timeout_us=200, congestion=True,
+                                       tick_us=500, entry_horizon_us=3000, exit_horizon_us=7000))
+    sched = [(170, 3000), (30, 300), (300, 3000)]
+    for label, kw in [("fixed", dict(coalesce_max_jobs=args.batch, coalesce_delay_us=500)),
+                      ("adaptive", dict(batching=rtmod.batching_config(
+                          "adaptive", 1, args.batch, coalesce_timeout_us=500, congestion=True, tick_us=500,
+                          entry_horizon_us=3000, exit_horizon_us=7000)))]:
+        key = f"resnet18_bs1_requests_bursty_schedule_{label}"
+        extras[key] = runtime_e2e(rtmod, replica, "resnet18", args.batch, 0, inflight=256, req_batch=1,
+                                  max_queue=256, schedule=sched, **kw)
+        extras[key]["schedule_delta_us_repeat"] = sched
+    if args.ci_schedule:
+        extras["ci_perf_resnet152_schedule"] = ci_perf_workload(spi, zoo, rtmod, dev, args.workers)
+    return extras
+
+
+def ci_perf_workload(spi, zoo, rtmod, dev, workers):
+    """The reference's own perf workload (.github/workflows/ci.yml:625-739 perf-smoke):
+    ResNet-152, bs1 requests on the ci/perf/ci_perf_resnet.csv schedule at its real intervals
+    (1700 us x 3000, 300 us x 300, 3000 us x 3000 = 6300 requests), served as
+    ci/perf/resnet152_ci_perf_gpu_only.yml configures it: adaptive batching 1..16, congestion
+    thresholds fill 0.85 / 0.65 with 3000 / 7000 ms horizons on a 500 ms tick, 10 ms coalesce
+    timeout, queue 100, pool of 12 slots, STARPU_CUDA_PIPELINE 4, 4 workers.  Precision fp16x3
+    (ResNet-152's parity-grade mode, C4)."""
+    m = zoo.build("resnet152", seed=0)
+    rep = spi.ModelReplica(m, dev, "fp16x3", max_batch=16, graphs=True)
+    sched = [(1700, 3000), (300, 300), (3000, 3000)]
+    b = rtmod.batching_config("adaptive", 1, 16, coalesce_timeout_us=10_000, congestion=True, tick_us=500_000,
+                              entry_horizon_us=3_000_000, exit_horizon_us=7_000_000, fill_high=0.85, fill_low=0.65)
+    out = runtime_e2e(rtmod, rep, "resnet152", 16, 0, inflight=256, req_batch=1, workers=workers, schedule=sched,
+                      max_queue=100, slots_per_device=12, pipeline_depth=4, batching=b)
+    out.update({"schedule_delta_us_repeat": sched, "expected_requests": 6300, "dtype": "fp16x3",
+                "config": "ci/perf/resnet152_ci_perf_gpu_only.yml (adaptive 1..16, queue 100, pool 12, pipeline 4)"})
+    del rep, m
+    return out
 
 
 if __name__ == "__main__":

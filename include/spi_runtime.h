@@ -158,14 +158,21 @@ typedef struct spi_runtime_config {
   int32_t pipeline_depth;     /* tasks in flight per worker (0 -> 2) */
   int32_t slots_per_device;   /* slot pool size per device (0 -> workers x depth) */
   int32_t copy_threads;       /* host staging threads incl. the worker (0 -> 4) */
-  int32_t h2d_mode;           /* enum spi_h2d_mode (default SPI_H2D_DEVICE_STREAM) */
+  int32_t h2d_mode;           /* enum spi_h2d_mode: spi_runtime_config_init sets SPI_H2D_AUTO; a
+                                 zeroed struct means SPI_H2D_DEVICE_STREAM (value 0) */
   int32_t min_priority;       /* starpu_sched_get_min_priority (0 with eager) */
   int32_t max_priority;       /* starpu_sched_get_max_priority (0 with eager) */
   spi_batching_config batching;
+  int32_t warmup_batches;     /* per-worker warm-up at create (inference_runner.cpp:507-560):
+                                 0 = every batch size 1..max_batch captured before serving (no
+                                 capture on a live request), k > 0 = batch sizes 1..k and max_batch,
+                                 -1 = max_batch only */
+  int32_t _pad0;
 } spi_runtime_config;
 
-/* Fills the defaults above (FIXED batching, one job per task).  A zeroed
- * struct means the same defaults. */
+/* Fills the defaults above (FIXED batching, one job per task, SPI_H2D_AUTO,
+ * every batch size warmed up).  A zeroed struct means the same, except the H2D
+ * mode: 0 is SPI_H2D_DEVICE_STREAM, only spi_runtime_config_init selects AUTO. */
 void spi_runtime_config_init(spi_runtime_config* config);
 
 spi_runtime* spi_runtime_create(const spi_runtime_config* config, char* err, size_t errlen);
@@ -195,6 +202,8 @@ int32_t spi_runtime_num_workers(const spi_runtime* rt);
  * staging (copy_job_inputs_to_slot), out[3] ns enqueueing H2D + codelet + D2H,
  * out[4] ns waiting on completion events.  Returns SPI_OK or an error status. */
 int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out);
+/* The H2D mode the runtime resolved (SPI_H2D_AUTO -> one of the concrete modes). */
+int32_t spi_runtime_h2d_mode(const spi_runtime* rt);
 /* Current adaptive target batch limit (samples); the fixed limit otherwise. */
 int32_t spi_runtime_batch_target(const spi_runtime* rt);
 void spi_runtime_destroy(spi_runtime* rt);

@@ -273,20 +273,35 @@ struct Worker {
 
 using QueueKey = std::pair<int64_t, uint64_t>;  // (-priority, submission sequence)
 
-// HIP device -> its HSA GPU agent (matched by PCI domain / bus / device) and the
-// first CPU agent, for SPI_H2D_WORKER_SDMA.  HIP has initialised HSA already.
-bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
+// HIP device -> its HSA GPU agent and the first CPU agent, for
+// SPI_H2D_WORKER_SDMA.  Matched by the agent UUID (hipDeviceGetUuid carries the
+// 16 hex digits of HSA_AMD_AGENT_INFO_UUID's body), so partitions of one GPU
+// that share a PCI bus / device (CPX / TPX modes) are told apart; without a
+// UUID, by PCI domain / bus / device / function, accepted only when exactly one
+// agent matches.  Resolved once per device and cached.  hsa_init / hsa_shut_down
+// are paired around the enumeration: HIP holds its own reference, which keeps
+// the agent handles valid for the process.
+bool resolve_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
+  hipUUID uuid{};
+  const bool have_uuid = hipDeviceGetUuid(&uuid, device) == hipSuccess;
   int bus = 0, dev = 0, dom = 0;
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, device) != hipSuccess)
     return false;
   struct Find {
+    char uuid[16];
+    bool have_uuid;
     uint32_t bdf, dom;
-    hsa_agent_t gpu{}, cpu{};
-    bool g = false, c = false;
-  } f{(uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom};
-  if (hsa_init() != HSA_STATUS_SUCCESS) return false;  // reference-counted; HIP holds one too
+    hsa_agent_t by_uuid{}, by_bdf{}, cpu{};
+    int n_uuid = 0, n_bdf = 0;
+    bool c = false;
+  } f{};
+  std::memcpy(f.uuid, uuid.bytes, 16);
+  f.have_uuid = have_uuid;
+  f.bdf = (uint32_t)((bus << 8) | (dev << 3));
+  f.dom = (uint32_t)dom;
+  if (hsa_init() != HSA_STATUS_SUCCESS) return false;
   hsa_iterate_agents(
       [](hsa_agent_t a, void* u) {
         Find& f = *static_cast<Find*>(u);
@@ -295,21 +310,53 @@ bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
         if (t == HSA_DEVICE_TYPE_CPU && !f.c) {
           f.cpu = a;
           f.c = true;
-        } else if (t == HSA_DEVICE_TYPE_GPU && !f.g) {
+        } else if (t == HSA_DEVICE_TYPE_GPU) {
+          char id[32] = {};
+          if (f.have_uuid && hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_UUID, id) == HSA_STATUS_SUCCESS &&
+              std::strncmp(id, "GPU-", 4) == 0 && std::strlen(id) >= 20 && std::memcmp(id + 4, f.uuid, 16) == 0) {
+            f.by_uuid = a;
+            ++f.n_uuid;
+          }
           uint32_t bdf = 0, dom = 0;
           hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
           hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
           if ((bdf & ~7u) == f.bdf && dom == f.dom) {
-            f.gpu = a;
-            f.g = true;
+            f.by_bdf = a;
+            ++f.n_bdf;
           }
         }
         return HSA_STATUS_SUCCESS;
       },
       &f);
-  gpu = f.gpu;
+  (void)hsa_shut_down();
   cpu = f.cpu;
-  return f.g && f.c;
+  if (f.n_uuid == 1) {
+    gpu = f.by_uuid;
+  } else if (f.n_uuid == 0 && f.n_bdf == 1) {
+    gpu = f.by_bdf;
+  } else {
+    return false;  // ambiguous (partitioned GPU without UUIDs): the stream H2D modes
+  }
+  return f.c;
+}
+
+bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
+  struct Entry {
+    bool ok;
+    hsa_agent_t gpu, cpu;
+  };
+  static std::mutex mu;
+  static std::map<int, Entry> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(device);
+  if (it == cache.end()) {
+    Entry e{};
+    e.ok = resolve_hsa_agents(device, e.gpu, e.cpu);
+    it = cache.emplace(device, e).first;
+  }
+  gpu = it->second.gpu;
+  cpu = it->second.cpu;
+  return it->second.ok;
 }
 
 }  // namespace
@@ -452,8 +499,17 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
         hsa_signal_subtract_screlease(w->h2d_signal, ni - i);
         break;
       }
-    hsa_signal_wait_scacquire(w->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                              sdma_wait_blocked ? HSA_WAIT_STATE_BLOCKED : HSA_WAIT_STATE_ACTIVE);
+    // A wait may return before the condition holds (the HSA spec allows it;
+    // ROCclr loops too): wait until the value drops below 1.  Each completed copy
+    // decrements it; a failed copy leaves it negative.
+    hsa_signal_value_t v = hsa_signal_load_scacquire(w->h2d_signal);
+    while (v >= 1)
+      v = hsa_signal_wait_scacquire(w->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                    sdma_wait_blocked ? HSA_WAIT_STATE_BLOCKED : HSA_WAIT_STATE_ACTIVE);
+    if (v < 0 && t.status == SPI_OK) {
+      t.status = SPI_ERR_DEVICE;
+      t.err = "SDMA H2D failed";
+    }
   }
   for (int i = 0; i < ni && t.status == SPI_OK && cfg.h2d_mode != SPI_H2D_WORKER_SDMA; ++i)
     if (hipMemcpyAsync(slot.d_in[i], slot.h_in[i], (size_t)t.total * in_sample_bytes[i], hipMemcpyHostToDevice,
@@ -833,13 +889,23 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       if (!wok) return cleanup_fail("stream creation failed for worker " + std::to_string(wid - 1));
     }
   }
-  // per-worker warm-up before serving: workspaces + graphs for max_batch
+  // Per-worker warm-up before serving (the reference warms every worker through the
+  // pipeline, inference_runner.cpp:507-560): the workspace and the graph of every batch
+  // size the batchers can compose, so no capture (serialised process-wide) or workspace
+  // allocation ever lands on a live request.
   const int64_t seq = cfg.input_ndims[0] >= 1 ? cfg.input_dims[0][0] : 0;
+  std::vector<int> warm;
+  if (cfg.warmup_batches >= 0) {
+    const int upto = cfg.warmup_batches == 0 ? cfg.max_batch : std::min(cfg.warmup_batches, cfg.max_batch);
+    for (int b = 1; b <= upto; ++b) warm.push_back(b);
+  }
+  if (warm.empty() || warm.back() != cfg.max_batch) warm.push_back(cfg.max_batch);
   for (auto& w : rt->workers) {
     (void)hipSetDevice(w->device);
-    if (spi_model_warmup(w->model, w->stream, cfg.max_batch, seq, cfg.num_inputs >= 2) != SPI_OK)
-      return cleanup_fail(std::string("warm-up failed for worker ") + std::to_string(w->worker_id) + ": " +
-                          spi_last_error());
+    for (int b : warm)
+      if (spi_model_warmup(w->model, w->stream, b, seq, cfg.num_inputs >= 2) != SPI_OK)
+        return cleanup_fail(std::string("warm-up failed for worker ") + std::to_string(w->worker_id) + " batch " +
+                            std::to_string(b) + ": " + spi_last_error());
   }
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
   if (const char* e = std::getenv("SPI_H2D_SDMA_WAIT"); e && std::strcmp(e, "blocked") == 0) rt->sdma_wait_blocked = true;
@@ -923,6 +989,8 @@ int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out
   out[4] = w.t_event.load();
   return SPI_OK;
 }
+
+int32_t spi_runtime_h2d_mode(const spi_runtime* rt) { return rt ? rt->cfg.h2d_mode : -1; }
 
 int32_t spi_runtime_batch_target(const spi_runtime* rt) {
   if (!rt) return 0;

@@ -73,6 +73,8 @@ class RuntimeConfig(C.Structure):
         ("min_priority", C.c_int32),
         ("max_priority", C.c_int32),
         ("batching", BatchingConfig),
+        ("warmup_batches", C.c_int32),
+        ("_pad0", C.c_int32),
     ]
 
 
@@ -111,6 +113,7 @@ for _name, _res, _args in [
     ("spi_runtime_num_workers", C.c_int32, [C.c_void_p]),
     ("spi_runtime_worker_times", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
     ("spi_runtime_batch_target", C.c_int32, [C.c_void_p]),
+    ("spi_runtime_h2d_mode", C.c_int32, [C.c_void_p]),
     ("spi_runtime_destroy", None, [C.c_void_p]),
     ("spi_runtime_loadgen", C.c_int, [C.c_void_p, C.POINTER(LoadgenConfig), C.POINTER(C.c_void_p),
                                       C.POINTER(LoadgenResult)]),
@@ -170,10 +173,12 @@ class Runtime:
                  workers_per_device: int = 4, max_queue: int = 0, coalesce_max_jobs: int = 1,
                  coalesce_delay_us: int = 0, pipeline_depth: int = 2, slots_per_device: int = 0,
                  copy_threads: int = 4, h2d_mode: str = "auto", min_priority: int = 0,
-                 max_priority: int = 0, batching: BatchingConfig | None = None):
+                 max_priority: int = 0, batching: BatchingConfig | None = None, warmup_batches: int = 0):
         """input_specs: [(per-sample shape, dtype)]; output_specs: [(per-sample elems, dtype)].
         Fixed batching (default): coalesce_max_jobs > 1 merges up to that many queued jobs (while
-        their samples fit max_batch), waiting up to coalesce_delay_us for more."""
+        their samples fit max_batch), waiting up to coalesce_delay_us for more.  warmup_batches: 0 =
+        every batch size 1..max_batch captured per worker before serving, k = 1..k and max_batch,
+        -1 = max_batch only."""
         cfg = RuntimeConfig()
         lib.spi_runtime_config_init(C.byref(cfg))
         cfg.num_devices = len(replicas)
@@ -192,6 +197,7 @@ class Runtime:
         cfg.min_priority, cfg.max_priority = min_priority, max_priority
         if batching is not None:
             cfg.batching = batching
+        cfg.warmup_batches = warmup_batches
         cfg.num_inputs = len(input_specs)
         self.input_specs = input_specs
         for i, (shape, dt) in enumerate(input_specs):
@@ -231,6 +237,12 @@ class Runtime:
             out.append(dict(tasks=v[0], slot_s=v[1] / 1e9, stage_s=v[2] / 1e9, enqueue_s=v[3] / 1e9,
                             event_s=v[4] / 1e9))
         return out
+
+    @property
+    def h2d_mode(self) -> str:
+        """The H2D mode in effect (SPI_H2D_AUTO resolved at create)."""
+        v = lib.spi_runtime_h2d_mode(self.handle)
+        return next(k for k, m in H2D_MODES.items() if m == v)
 
     @property
     def batch_target(self) -> int:

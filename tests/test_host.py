@@ -62,3 +62,21 @@ def test_shard_requests_is_a_partition():
     for world in (1, 2, 3, 8):
         got = sorted(i for r in range(world) for i in bench.shard_requests(37, r, world))
         assert got == list(range(37))
+
+
+def test_bench_gpus_2_spawns_two_ranks_control_path():
+    """`python bench.py --gpus 2` (no launcher): two rank processes through the real control path
+    (spawn_ranks, gloo rendezvous, barrier + max-over-ranks timing, e2e aggregation); the JSON
+    line must say n_gpus 2 and carry the slowest rank's window."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                          "--control-plane-only"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    assert line["ms_per_step"] >= 2.0  # rank 1 sleeps 2 ms per step: the max over ranks
+    e = line["e2e"]
+    assert e["requests"] == 200 and abs(e["seconds"] - 0.2) < 1e-9 and e["p50_latency_ms"] == 2.0
+    assert abs(e["value"] - 200 * 8 / 0.2) < 1e-6 and len(e["per_rank"]) == 2

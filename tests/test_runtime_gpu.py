@@ -57,7 +57,9 @@ def test_runtime_bert_two_inputs(spi, zoo, rtmod, h2d):
     rt.submit(7, [ids, mask], [out])
     rt.drain()
     assert rt.completions[0].status == 0
-    assert normalized_max_error(out, cpu_inference(m, [ids, mask])[0]) < 2e-3
+    err = normalized_max_error(out, cpu_inference(m, [ids, mask])[0])
+    print(f"runtime bert L2 S32 fp16 {h2d} err={err:.3e}")
+    assert err < 1e-3
     rt.close()
 
 
@@ -167,7 +169,7 @@ def test_runtime_two_replicas_on_one_device(spi, zoo, rtmod):
     rt.close()
 
 
-@pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy"])
+@pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy", "worker_sdma"])
 def test_runtime_pipeline_with_small_slot_pool(spi, zoo, rtmod, h2d_mode):
     """Pipeline depth 3 per worker over a 2-slot pool (fewer slots than workers x depth): the
     worker must finalize its own finished tasks to free slots (SlotPoolBase::try_acquire /

@@ -1,0 +1,200 @@
+"""GPU parity at the shapes the serving path actually runs (VERDICT r02 "What's missing" 2).
+
+* ResNet-18 bs=1 at 224 -- the shape BASELINE's metric names -- in fp32 / fp16m / fp16x3,
+  through the C-ABI, against the reference-style LibTorch CPU codelet (libspi_torch.so:
+  spi_cpu_inference_func over the same TorchScript .pt, starpu_setup.cpp:784-801) on the
+  SAME inputs; the CPU codelet's own C1 run (configs[0]) is checked here too, so the
+  GPU-box test run carries C1.
+* Every task batch 1..8 at 224 in fp16m: what the fixed and adaptive batchers compose
+  (dims[0] = effective batch, inference_task.cpp:606-613; batching_strategy.cpp:195-360).
+* The runtime's production path (SPI_H2D_AUTO -> SDMA H2D, fused stem reading d_in, 224
+  bs8, 4 workers x depth 2) with a distinct input per job, and bs1 requests under the
+  adaptive batcher, every job's rows checked against the oracle.
+* A scripted (torch.jit.script) ViT .pt, the reference's default export
+  (models/import_vit.py:41-55), through ModelReplica(path).
+
+Bars (BASELINE north_star): 1e-5 fp32 (and fp16x3, fp32-grade), 1e-3 fp16 / fp16m, as the
+normalised max error max|hip - ref| / max|ref|, plus top-1 agreement for classifiers.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_codelet import cpu_inference, normalized_max_error, top1_agreement
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": 1e-5, "fp16x3": 1e-5, "fp16m": 1e-3, "fp16": 1e-3}
+
+
+def hip(spi, rep, inputs, shape, graphs=True):
+    ins = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in inputs]
+    out = torch.full(shape, float("nan"), device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    rep.set_graphs(graphs)
+    spi.run_hip(rep, ins, out, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def resnet18_pt(zoo, tmp_path_factory):
+    m = zoo.resnet18()
+    path = str(tmp_path_factory.mktemp("serving") / "resnet18.pt")
+    torch.jit.trace(m, torch.rand(1, 3, 224, 224)).save(path)
+    return m, path
+
+
+@pytest.fixture(scope="module")
+def lt(spi):
+    return importlib.import_module("starpu-inference-server_amd.libtorch")
+
+
+def cpu_codelet_forward(spi, lt, path, x):
+    """spi_cpu_inference_func over the TorchScript module (the reference's cpu_inference_func)."""
+    ts = lt.TorchScriptModule(path)
+    out = np.full((x.shape[0], 1000), np.nan, dtype=np.float32)
+    params = spi.make_params([list(x.shape)], [torch.float32], num_outputs=1, model_cpu=ts)
+    bufs = [spi.tensor_interface(torch.from_numpy(x)), spi.tensor_interface(torch.from_numpy(out))]
+    with spi.worker_context(3, -1, None):
+        args = spi.InferenceCodelet.cpu_inference_func(bufs, params)
+    ts.close()
+    return out, args
+
+
+def test_c1_resnet18_bs1_fp32_cpu_codelet_on_gpu_box(spi, lt, gpu, resnet18_pt):
+    """BASELINE configs[0] on the GPU box's host: ResNet-18 bs=1 fp32 through the C++ CPU
+    codelet (TorchScript), against the Python ATen oracle on the same module."""
+    _, path = resnet18_pt
+    x = np.random.default_rng(0).random((1, 3, 224, 224), dtype=np.float32)
+    out, args = cpu_codelet_forward(spi, lt, path, x)
+    ref = cpu_inference(torch.jit.load(path), [x])[0]
+    err = normalized_max_error(out, ref)
+    print(f"C1 cpu codelet vs oracle err={err:.3e}")
+    assert err < 1e-6 and args.status == 0 and args.executed_on == spi._native.DEVICE_CPU
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16m", "fp16x3"])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_resnet18_bs1_224_hip_vs_cpu_codelet(spi, lt, gpu, resnet18_pt, prec, seed):
+    """The metric's shape: ResNet-18 bs=1 at 224, HIP codelet (replica loaded from the .pt)
+    vs the LibTorch CPU codelet on identical TorchScript inputs."""
+    _, path = resnet18_pt
+    x = np.random.default_rng(100 + seed).random((1, 3, 224, 224), dtype=np.float32)
+    ref, _ = cpu_codelet_forward(spi, lt, path, x)
+    rep = spi.ModelReplica(path, 0, prec, max_batch=1, graphs=True)
+    got = hip(spi, rep, [x], ref.shape)
+    got_eager = hip(spi, rep, [x], ref.shape, graphs=False)
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@224 bs1 {prec} seed{seed} err={err:.3e}")
+    assert np.isfinite(got).all()
+    assert err < TOL[prec]
+    assert top1_agreement(got, ref) == 1.0
+    np.testing.assert_array_equal(got, got_eager)  # graph replay == eager launches
+
+
+@pytest.fixture(scope="module")
+def r18_fp16m_b8(spi, zoo, gpu):
+    m = zoo.resnet18()
+    return m, spi.ModelReplica(m, 0, "fp16m", max_batch=8, graphs=True)
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_resnet18_fp16m_224_every_task_batch(spi, gpu, r18_fp16m_b8, batch):
+    """Every effective batch a batcher can hand the codelet (one max_batch=8 replica, graphs
+    per batch size), fp16m at 224 against the fp32 oracle."""
+    m, rep = r18_fp16m_b8
+    x = np.random.default_rng(200 + batch).random((batch, 3, 224, 224), dtype=np.float32)
+    ref = cpu_inference(m, [x])[0]
+    got = hip(spi, rep, [x], ref.shape)
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@224 fp16m B={batch} err={err:.3e}")
+    assert err < TOL["fp16m"]
+    assert top1_agreement(got, ref) == 1.0
+
+
+@pytest.fixture(scope="module")
+def rtmod(spi, gpu):
+    return importlib.import_module("starpu-inference-server_amd.runtime")
+
+
+def test_runtime_production_path_sdma_distinct_inputs(spi, rtmod, r18_fp16m_b8):
+    """ResNet-18 fp16m at 224, bs8 jobs, 4 workers x depth 2, H2D AUTO (resolves to the SDMA
+    engines for this link-bound model): 4 x slots_per_device jobs, each with its own input,
+    so a stale or early read of a reused slot would show as a wrong job."""
+    m, rep = r18_fp16m_b8
+    rt = rtmod.Runtime([rep], [((3, 224, 224), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=4,
+                       pipeline_depth=2, h2d_mode="auto")
+    try:
+        assert rt.h2d_mode == "worker_sdma"
+        rng = np.random.default_rng(300)
+        jobs = []
+        for rid in range(4 * 8):  # slots_per_device = workers x depth = 8
+            x = rng.random((8, 3, 224, 224), dtype=np.float32)
+            y = np.full((8, 1000), np.nan, dtype=np.float32)
+            rt.submit(rid, [x], [y])
+            jobs.append((x, y))
+        rt.drain()
+        assert rt.stats() == (32, 0)
+        xs = np.concatenate([x for x, _ in jobs])
+        ys = np.concatenate([y for _, y in jobs])
+        ref = cpu_inference(m, [xs])[0]
+        errs = [normalized_max_error(ys[i * 8:(i + 1) * 8], ref[i * 8:(i + 1) * 8]) for i in range(len(jobs))]
+        print(f"runtime sdma fp16m bs8 x32 max err={max(errs):.3e}")
+        assert max(errs) < TOL["fp16m"]
+        assert top1_agreement(ys, ref) == 1.0
+        assert len({c.worker_id for c in rt.completions}) >= 2
+    finally:
+        rt.close()
+
+
+def test_runtime_bs1_requests_adaptive_every_task_size(spi, rtmod, r18_fp16m_b8):
+    """bs1 requests under the adaptive batcher at 224 fp16m: the runtime composes tasks of
+    several sizes; every request's row must match its own image's forward."""
+    m, rep = r18_fp16m_b8
+    b = rtmod.batching_config("adaptive", min_batch=1, batch_limit=8, coalesce_timeout_us=300, congestion=True,
+                              tick_us=100, entry_horizon_us=400, exit_horizon_us=2000)
+    rt = rtmod.Runtime([rep], [((3, 224, 224), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=4,
+                       max_queue=256, batching=b)
+    try:
+        rng = np.random.default_rng(400)
+        n = 96
+        xs = [rng.random((1, 3, 224, 224), dtype=np.float32) for _ in range(n)]
+        ys = [np.full((1, 1000), np.nan, dtype=np.float32) for _ in range(n)]
+        for i in range(n):
+            rt.submit(i, [xs[i]], [ys[i]])
+            if i % 24 == 23:
+                rt.drain()  # bursts: the target moves, task sizes vary
+        rt.drain()
+        assert rt.stats() == (n, 0)
+        ref = cpu_inference(m, [np.concatenate(xs)])[0]
+        got = np.concatenate(ys)
+        err = normalized_max_error(got, ref)
+        sizes = sorted({c.task_batch for c in rt.completions})
+        print(f"runtime bs1 adaptive fp16m err={err:.3e} task sizes={sizes}")
+        assert err < TOL["fp16m"]
+        assert top1_agreement(got, ref) == 1.0
+        assert len(sizes) >= 2
+    finally:
+        rt.close()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_scripted_vit_pt(spi, zoo, gpu, tmp_path, prec):
+    """models/import_vit.py exports with torch.jit.script by default (:41-55): a scripted ViT
+    .pt through ModelReplica(path), against the CPU codelet oracle on the loaded module."""
+    m = zoo.vit(image=224, patch=16, layers=2, heads=2, dim=128, mlp_dim=256)
+    path = str(tmp_path / "vit_scripted.pt")
+    torch.jit.script(m).save(path)
+    loaded = spi.load_model(path)
+    x = np.random.default_rng(500).random((2, 3, 224, 224), dtype=np.float32)
+    ref = cpu_inference(loaded, [x])[0]
+    rep = spi.ModelReplica(path, 0, prec, max_batch=2)
+    got = hip(spi, rep, [x], ref.shape, graphs=False)
+    err = normalized_max_error(got, ref)
+    print(f"scripted vit .pt {prec} err={err:.3e}")
+    assert err < TOL[prec]
+    assert top1_agreement(got, ref) == 1.0
