@@ -290,6 +290,9 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
            "requests": r["completed"], "request_batch": rb, "max_batch": batch, "inflight": inflight,
            "workers": workers, "mean_task_batch": round(r["mean_task_batch"], 2),
            "p50_queue_ms": round(r["p50_queue_ms"], 4), "failed": r["failed"], "rejected": r["rejected"],
+           "breakdown_ms": {k: round(r[k], 4) for k in ("p99_queue_ms", "p50_stage_ms", "p99_stage_ms",
+                                                        "p50_device_ms", "p99_device_ms", "max_ms")},
+           "worst_request_at": round(r["worst_at_frac"], 3),
            "seconds": round(r["seconds"], 3), "h2d_mode": h2d}
     if r["error"]:
         out["first_error"] = r["error"]

@@ -241,6 +241,11 @@ typedef struct spi_loadgen_result {
   double p50_ms, p95_ms, p99_ms, mean_ms, max_ms;
   double mean_jobs_per_task, mean_task_batch;
   double p50_queue_ms;       /* submit -> dequeue */
+  /* latency breakdown (CLOCK_MONOTONIC stamps of spi_job_timing): queue = submit -> dequeue,
+     stage = dequeue -> codelet start (slot, host staging, H2D), device = codelet start ->
+     outputs in the caller's buffers (kernels, D2H, completion wait, slicing) */
+  double p99_queue_ms, p50_stage_ms, p99_stage_ms, p50_device_ms, p99_device_ms;
+  double worst_at_frac;      /* submit time of the slowest request, as a fraction of the run */
   char error[SPI_ERROR_LEN];
 } spi_loadgen_result;
 

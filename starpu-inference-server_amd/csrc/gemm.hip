@@ -1569,7 +1569,9 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   check_desc(d, prec);
   switch (prec) {
     case Prec::F16:
-      if (gemm256_eligible(d, prec, knobs().g256_min) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
+      if (conv_wres_eligible(d, prec, p))
+        conv_wres(d, p, s);
+      else if (gemm256_eligible(d, prec, knobs().g256_min) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
           (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
         gemm256(d, p, s);
       else

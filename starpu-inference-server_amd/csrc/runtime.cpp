@@ -370,6 +370,9 @@ struct spi_runtime {
   // SPI_H2D_SDMA_WAIT=blocked: the worker thread sleeps on the SDMA completion signal
   // instead of polling it (read at create)
   bool sdma_wait_blocked = false;
+  // SPI_RT_COMPLETION=spin: finalize polls the completion event (yielding) instead of
+  // hipEventSynchronize (read at create)
+  bool spin_completion = false;
   std::mutex mu;
   std::condition_variable cv_job, cv_idle;
   std::map<QueueKey, Job> queue;
@@ -598,7 +601,13 @@ void spi_runtime::finalize_oldest(Worker* w) {
   SlotPool& pool = *pools[w->pool];
   Slot& slot = pool.slots[t.slot];
   const int64_t e0 = now_ns();
-  if (hipEventSynchronize(slot.done) != hipSuccess && t.status == SPI_OK) {
+  hipError_t se;
+  if (spin_completion) {
+    while ((se = hipEventQuery(slot.done)) == hipErrorNotReady) std::this_thread::yield();
+  } else {
+    se = hipEventSynchronize(slot.done);
+  }
+  if (se != hipSuccess && t.status == SPI_OK) {
     t.status = SPI_ERR_DEVICE;
     t.err = "stream synchronisation failed";
   }
@@ -909,6 +918,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   }
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
   if (const char* e = std::getenv("SPI_H2D_SDMA_WAIT"); e && std::strcmp(e, "blocked") == 0) rt->sdma_wait_blocked = true;
+  if (const char* e = std::getenv("SPI_RT_COMPLETION"); e && std::strcmp(e, "spin") == 0) rt->spin_completion = true;
   rt->last_target = cfg.max_batch;
   for (auto& w : rt->workers) w->thread = std::thread(&spi_runtime::run, rt.get(), w.get());
   return rt.release();
@@ -1019,7 +1029,7 @@ void spi_runtime_destroy(spi_runtime* rt) {
 namespace {
 struct LoadGen {
   struct Req {
-    int64_t submit = 0, complete = 0, dequeue = 0;
+    int64_t submit = 0, complete = 0, dequeue = 0, cstart = 0;
     int32_t status = -1, jobs = 0, batch = 0;
     int buf = -1;
     LoadGen* gen = nullptr;
@@ -1037,6 +1047,7 @@ struct LoadGen {
     LoadGen* g = r->gen;
     r->complete = t->complete_ns;
     r->dequeue = t->dequeue_ns;
+    r->cstart = t->codelet_start_ns;
     r->status = status;
     r->jobs = t->task_jobs;
     r->batch = t->task_batch;
@@ -1145,8 +1156,8 @@ int spi_runtime_loadgen(spi_runtime* rt, const spi_loadgen_config* c, const void
       }
   }
   spi_runtime_drain(rt);
-  std::vector<double> lat, qlat;
-  int64_t first = INT64_MAX, last = 0, ok = 0, bad = 0;
+  std::vector<double> lat, qlat, slat, dlat;
+  int64_t first = INT64_MAX, last = 0, ok = 0, bad = 0, worst_submit = 0;
   double jobs = 0, batch = 0, sum = 0, mx = 0;
   for (auto& r : g.reqs) {
     if (r.status == SPI_ERR_QUEUE_FULL) continue;
@@ -1160,13 +1171,18 @@ int spi_runtime_loadgen(spi_runtime* rt, const spi_loadgen_config* c, const void
     const double ms = (r.complete - r.submit) * 1e-6;
     lat.push_back(ms);
     qlat.push_back((r.dequeue - r.submit) * 1e-6);
+    slat.push_back((r.cstart - r.dequeue) * 1e-6);
+    dlat.push_back((r.complete - r.cstart) * 1e-6);
     sum += ms;
+    if (ms > mx) worst_submit = r.submit;
     mx = std::max(mx, ms);
     jobs += r.jobs;
     batch += r.batch;
   }
   std::sort(lat.begin(), lat.end());
   std::sort(qlat.begin(), qlat.end());
+  std::sort(slat.begin(), slat.end());
+  std::sort(dlat.begin(), dlat.end());
   res->completed = ok;
   res->failed = bad;
   res->rejected = rejected;
@@ -1181,6 +1197,12 @@ int spi_runtime_loadgen(spi_runtime* rt, const spi_loadgen_config* c, const void
   res->mean_jobs_per_task = ok ? jobs / ok : 0;
   res->mean_task_batch = ok ? batch / ok : 0;
   res->p50_queue_ms = pct(qlat, 50);
+  res->p99_queue_ms = pct(qlat, 99);
+  res->p50_stage_ms = pct(slat, 50);
+  res->p99_stage_ms = pct(slat, 99);
+  res->p50_device_ms = pct(dlat, 50);
+  res->p99_device_ms = pct(dlat, 99);
+  res->worst_at_frac = ok && last > first ? (double)(worst_submit - first) / (double)(last - first) : 0.0;
   std::snprintf(res->error, SPI_ERROR_LEN, "%s", g.first_err.c_str());
   return bad ? SPI_ERR_DEVICE : SPI_OK;
 }

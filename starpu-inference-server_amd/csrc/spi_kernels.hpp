@@ -84,6 +84,12 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
 void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
 
+// Weight-resident 3x3/s1/p1 conv, 64 -> 64 channels, fp16 NHWC (conv_wres.hip): the
+// folded weights stay in LDS while a workgroup walks bands of output rows; gemm()
+// routes an eligible desc to it (SPI_CONV_WRES=0: never).
+bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p);
+void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
+
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
                  bool f16, hipStream_t s);

@@ -99,7 +99,9 @@ class LoadgenResult(C.Structure):
                 ("inferences", C.c_int64), ("seconds", C.c_double), ("inferences_per_s", C.c_double),
                 ("p50_ms", C.c_double), ("p95_ms", C.c_double), ("p99_ms", C.c_double), ("mean_ms", C.c_double),
                 ("max_ms", C.c_double), ("mean_jobs_per_task", C.c_double), ("mean_task_batch", C.c_double),
-                ("p50_queue_ms", C.c_double), ("error", C.c_char * N.SPI_ERROR_LEN)]
+                ("p50_queue_ms", C.c_double), ("p99_queue_ms", C.c_double), ("p50_stage_ms", C.c_double),
+                ("p99_stage_ms", C.c_double), ("p50_device_ms", C.c_double), ("p99_device_ms", C.c_double),
+                ("worst_at_frac", C.c_double), ("error", C.c_char * N.SPI_ERROR_LEN)]
 
 
 for _name, _res, _args in [
