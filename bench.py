@@ -282,7 +282,8 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
     rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers,
                        **kw)
     h2d = rt.h2d_mode
-    r = rt.loadgen(host_inputs, requests=requests, inflight=inflight, warmup=4 * workers * 2, schedule=schedule)
+    r = rt.loadgen(host_inputs, requests=requests, inflight=inflight, warmup=max(8 * workers, 2 * inflight),
+                   schedule=schedule)
     target = rt.batch_target
     rt.close()
     out = {"value": round(r["inferences_per_s"], 2), "unit": "inferences/s", "p50_latency_ms": round(r["p50_ms"], 4),

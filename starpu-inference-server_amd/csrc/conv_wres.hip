@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 namespace spi {
 namespace {
@@ -42,22 +43,25 @@ constexpr int kWImg = 64 * kRowB;           // one tap's [64 cout][64 cin] image
 constexpr int kWBytes = 9 * kWImg;          // 72 KiB resident weights
 constexpr int kHaloPix = 256;               // halo buffer capacity in pixels
 constexpr int kHBuf = kHaloPix * kRowB;     // 32 KiB (also the 128 x 64 fp32 epilogue tile)
-constexpr int kLds = kWBytes + 2 * kHBuf;   // 136 KiB: one workgroup per CU
+// LDS: NBUF halo buffers (2: the next band's halo streams in during this band's k-loop;
+// 1: one band per workgroup) + the resident weights -- 136 / 104 KiB.  With one buffer a
+// 48 KiB workgroup of another worker stream's kernel still fits beside it on the CU.
+template <int NBUF>
+constexpr int kLds = NBUF * kHBuf + kWBytes;
 constexpr int BM = 128, BN = 64, NT = 256;  // tile rows (pixels of a band), columns, threads
 constexpr int kWPieces = kWBytes / 1024 / 4;   // 18 weight DMA pieces per wave
 constexpr int kHPieces = kHBuf / 1024 / 4;     // 8 halo DMA pieces per wave
 
 struct WresArgs {
   const _Float16* x;    // [B][H][W][64]
-  const char* w;        // packed [128][576] fp16 (pack_conv: k = tap * 64 + c), bias folded separately
-  const float* bias;    // [64]
+  const char* w;        // packed [128][576] fp16: rows 0..63 the matrix, rows 64..127 the LDS image
+  const float* bias;    // [64] (the zero line when the conv has none)
   const _Float16* res;  // [B][H][W][64] or nullptr
   _Float16* y;          // [B][H][W][64]
-  const char* zeros;    // >= 16 zero bytes
+  const char* zeros;    // >= 256 zero bytes
   int H, W;             // input = output size
   int th;               // output rows per band
   int bands_per_img, bands, bpw;
-  int relu;
 };
 
 __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
@@ -71,22 +75,63 @@ __device__ __forceinline__ void dma_wait_barrier() {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// One 1-KiB LDS-DMA piece (lane l's 16 bytes from `src` to dst + 16 l), issued in
+// inline asm so hipcc does not track it: with the builtin, hipcc cannot tell the
+// pending DMA from the LDS the next ds_reads touch and drains every DMA
+// (s_waitcnt vmcnt(0)) before them, which would serialise the next band's halo with
+// this band's k-loop.  The caller counts these with dma_wait_barrier<N>
+// (cdna_hip_programming.md 5.7, the M0-saving LDS-DMA recipe).
+__device__ __forceinline__ void glds16(const void* src, const char* dst) {
+  const lds_ptr_t lp = (lds_ptr_t)(const_cast<char*>(dst));
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lp);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(m0v)
+               : "memory");
+}
+
+// Diagnostic build (-DSPI_WRES_STAMPS): per-workgroup s_memtime stamps of the phases of
+// its first two bands (tools/wres_stamps.py); no output value depends on them.
+#ifdef SPI_WRES_STAMPS
+__device__ unsigned long long g_wres_stamps[4096 * 10];
+#define WRES_STAMP(k)                                                                   \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    if (tid == 0 && blockIdx.x < 4096) g_wres_stamps[blockIdx.x * 10 + (k)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+  } while (0)
+#else
+#define WRES_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
+// LDS map: halo buffers at 0 and kHBuf (A fragment reads then use an immediate
+// offset per buffer), the resident weights from 2 * kHBuf.
+
+template <bool HAS_RES, bool RELU, int NBUF>
 __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  constexpr int kW0 = NBUF * kHBuf;
+  __shared__ __attribute__((aligned(16))) char lds[kLds<NBUF>];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b_first = blockIdx.x * a.bpw;
   const int nb = min(a.bpw, a.bands - b_first);
   if (nb <= 0) return;  // uniform per workgroup
   const int Wp = a.W + 2;
   const int hp = (a.th + 2) * Wp;
+#ifdef SPI_WRES_STAMPS
+  if (tid == 0 && blockIdx.x < 4096) g_wres_stamps[blockIdx.x * 10 + 9] = __builtin_amdgcn_s_memrealtime();
+#endif
+  WRES_STAMP(0);
 
-  // ---- resident weights: 72 pieces of 1 KiB (8 rows x 128 B of one tap), 18 per wave
+  // ---- resident weights: the packed matrix's padding rows hold the LDS image (pack.hpp:
+  // pack_matrix_into), 72 contiguous pieces of 1 KiB, 18 per wave
+  const char* wimg = a.w + (size_t)64 * (9 * kRowB);
 #pragma unroll
   for (int i = 0; i < kWPieces; ++i) {
     const int q = wave * kWPieces + i;
-    const int tap = q >> 3, n = ((q & 7) << 3) + (lane >> 3), c = (lane & 7) ^ (n & 7);
-    const char* src = a.w + (size_t)n * (9 * kRowB) + tap * kRowB + c * 16;
-    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(lds + q * 1024), 16, 0, 0);
+    glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
   }
 
   // ---- halo bookkeeping, band-independent: piece i of this wave fills pixels
@@ -105,66 +150,130 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   auto issue_halo = [&](int band, int buf) {
     const int img = band / a.bands_per_img, oy0 = (band - img * a.bands_per_img) * a.th;
     const _Float16* base = a.x + ((size_t)img * a.H + oy0) * a.W * 64;
-    char* dst = lds + kWBytes + buf * kHBuf;
+    char* dst = lds + buf * kHBuf;
 #pragma unroll
     for (int i = 0; i < kHPieces; ++i) {
       const int iy = oy0 - 1 + h_hy[i];
       const bool ok = h_ok[i] && (unsigned)iy < (unsigned)a.H;
       const char* src = ok ? reinterpret_cast<const char*>(base + h_off[i]) : a.zeros;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(dst + (wave * kHPieces + i) * 1024), 16, 0, 0);
+      glds16(src, dst + (wave * kHPieces + i) * 1024);
     }
   };
 
-  // ---- fragment rows: wave (wm, wn) owns tile rows wm * 64 .. + 63 (TI = 4 blocks)
-  // x columns wn * 32 .. + 31 (TJ = 2); tile row r = output pixel (ty, tx) of the band
+  // ---- fragment addresses, band-independent.  Wave (wm, wn) owns tile rows wm * 64 .. + 63
+  // (TI = 4 blocks) x columns wn * 32 .. + 31 (TJ = 2); tile row r = output pixel (ty, tx) of
+  // the band.  k-chunk t = (tap, kk): 32 channels kk * 32 .. of tap t / 2; the lane reads 16-byte
+  // chunk kk * 4 + fq.  A: halo pixel of the row at tap (kh, kw), swizzled slot; B: tap image row.
   const int fr = lane & 15, fq = lane >> 4, wm = wave >> 1, wn = wave & 1;
-  int h_row[4];
+  int aoff[9][2][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = wm * 64 + i * 16 + fr;
     const int ty = r / a.W, tx = r - ty * a.W;
-    h_row[i] = ty < a.th ? ty * Wp + tx : 0;  // rows past the band read pixel 0, never stored
+    const int p0 = ty < a.th ? ty * Wp + tx : 0;  // rows past the band read pixel 0, never stored
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int p = p0 + (tap / 3) * Wp + tap % 3;
+        aoff[tap][kk][i] = p * kRowB + (((kk * 4 + fq) ^ (p & 7)) << 4);
+      }
+  }
+  int boff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int n = wn * 32 + jj * 16 + fr;
+      boff[kk][jj] = kW0 + n * kRowB + (((kk * 4 + fq) ^ (n & 7)) << 4);
+    }
+
+  // Epilogue bookkeeping, band-independent: thread -> 8-column group e_nb8, tile rows
+  // e_r0 + it * 32; e_rel = pixel offset of the row inside the band, e_ty its output row
+  // (>= th: a padding row, never stored).  The bias is read as two 16-byte loads (a.bias is
+  // never null: the host points it at the zero line) -- per-element guarded loads had made
+  // hipcc wait on eight dependent L2 round trips per band.
+  constexpr int E_G = BN / 8, E_RSTEP = NT / E_G, E_ITEMS = BM / E_RSTEP;  // 8 groups, rows 32 apart, 4 rows
+  const int e_nb8 = (tid % E_G) * 8, e_r0 = tid / E_G;
+  int e_rel[E_ITEMS], e_ty[E_ITEMS];
+#pragma unroll
+  for (int it = 0; it < E_ITEMS; ++it) {
+    const int row = e_r0 + it * E_RSTEP;
+    const int ty = row / a.W, tx = row - ty * a.W;
+    e_ty[it] = ty < a.th ? ty : 1 << 30;
+    e_rel[it] = ty * a.W + tx;
   }
 
-  issue_halo(b_first, 0);
-  for (int j = 0; j < nb; ++j) {
-    const int band = b_first + j;
-    const bool next = j + 1 < nb;
-    if (next) issue_halo(band + 1, (j + 1) & 1);  // the buffer band j - 1 used (its epilogue ended in a barrier)
+  // One band on halo buffer BUF (a compile-time constant: every fragment read is a VGPR
+  // address plus an immediate).  The k-loop keeps chunk t + 1's six fragment reads in
+  // flight behind chunk t's eight MFMAs (sched_barrier pins the order; the compiler's
+  // counted lgkmcnt then waits only for chunk t).
+  auto band_body = [&](auto buf_c, int band, bool next, int sk) {
+    const bool more = next;
+    constexpr int BUF = decltype(buf_c)::value;
+    // the next band's halo into the buffer band - 1 used (its epilogue ended in a barrier); one
+    // buffer: only after this band's epilogue
+    if (NBUF == 2 && next) issue_halo(band + 1, BUF ^ 1);
+    if (NBUF == 1) next = false;
     if (next)
       dma_wait_barrier<kHPieces>();  // everything but the next halo has landed
     else
       dma_wait_barrier<0>();
-    const char* Hs = lds + kWBytes + (j & 1) * kHBuf;
+    if (sk >= 0) WRES_STAMP(sk);
+    const char* Hs = lds + BUF * kHBuf;
 
     floatx4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
+    half8 fa[2][4], fb[2][2];
+    auto load = [&](int t, int s) {
+      const int tap = t >> 1, kk = t & 1;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int toff = (tap / 3) * Wp + tap % 3;
-      const char* Ws = lds + tap * kWImg;
+      for (int i = 0; i < 4; ++i) fa[s][i] = *reinterpret_cast<const half8*>(Hs + aoff[tap][kk][i]);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        half8 af[4], bf[2];
+      for (int jj = 0; jj < 2; ++jj)
+        fb[s][jj] = *reinterpret_cast<const half8*>(lds + boff[kk][jj] + tap * kWImg);
+    };
+    load(0, 0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = __builtin_bit_cast(half8, rd_chunk(Hs, h_row[i] + toff, kk * 4 + fq));
+    for (int t = 0; t < 18; ++t) {
+      if (t + 1 < 18) load(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          bf[jj] = __builtin_bit_cast(half8, rd_chunk(Ws, wn * 32 + jj * 16 + fr, kk * 4 + fq));
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t & 1][i], fb[t & 1][jj], acc[i][jj], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (sk >= 0) WRES_STAMP(sk + 1);
+
+    // ---- epilogue through this band's halo buffer (every wave is done reading it).  The
+    // residual rows go out first (clamped rows: always-valid addresses, no branch), so their
+    // latency hides behind the park; HAS_RES / RELU are template parameters -- a runtime
+    // `if (res)` per row had made hipcc branch around each load and wait vmcnt(0) per row.
+    const int img = band / a.bands_per_img, oy0 = (band - img * a.bands_per_img) * a.th;
+    const int rows_left = a.H - oy0;  // output rows of this band inside the image
+    const size_t mbase = ((size_t)img * a.H + oy0) * a.W;
+    // the bias here rather than once per workgroup: a load pending across the k-loop makes
+    // hipcc drain every vector-memory operation (vmcnt(0)) before the loop's first ds_read
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(a.bias + e_nb8);
+    const floatx4 b1 = *reinterpret_cast<const floatx4*>(a.bias + e_nb8 + 4);
+    half8 rv[E_ITEMS];
+    if constexpr (HAS_RES) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[jj], acc[i][jj], 0, 0, 0);
+      for (int it = 0; it < E_ITEMS; ++it) {
+        const size_t mm = mbase + (e_ty[it] < rows_left ? e_rel[it] : 0);
+        rv[it] = *reinterpret_cast<const half8*>(a.res + mm * 64 + e_nb8);
       }
     }
-
-    // ---- epilogue through this band's halo buffer (every wave is done reading it)
     lds_barrier();
-    float* T = reinterpret_cast<float*>(lds + kWBytes + (j & 1) * kHBuf);
+#ifdef SPI_WRES_STAMPS_EPI
+    if (sk == 1) WRES_STAMP(4);
+#endif
+    float* T = reinterpret_cast<float*>(lds + BUF * kHBuf);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -175,49 +284,54 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
           const int col = (wn * 32 + jj * 16 + fr) ^ (fq << 4);  // (row >> 2) & 3 == fq
           T[row * BN + col] = acc[i][jj][r];
         }
+#ifdef SPI_WRES_STAMPS_EPI
+    if (sk == 1) WRES_STAMP(5);
+#endif
     lds_barrier();
-    {
-      constexpr int G = BN / 8, RSTEP = NT / G, ITEMS = BM / RSTEP;  // 8 column groups, 32 rows apart, 4 rows
-      const int cg = tid % G, r0 = tid / G, nb8 = cg * 8;
-      const int img = band / a.bands_per_img, oy0 = (band - img * a.bands_per_img) * a.th;
-      float bv[8];
+#ifdef SPI_WRES_STAMPS_EPI
+    if (sk == 1) WRES_STAMP(6);
+#endif
+    half8 hv[E_ITEMS];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bv[e] = a.bias[nb8 + e];
-      int m[ITEMS];
-      float yv[ITEMS][8];
+    for (int it = 0; it < E_ITEMS; ++it) {
+      const int row = e_r0 + it * E_RSTEP;
+      const float* src = T + row * BN + (e_nb8 ^ (((row >> 2) & 3) << 4));
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
 #pragma unroll
-      for (int it = 0; it < ITEMS; ++it) {
-        const int row = r0 + it * RSTEP;
-        const int ty = row / a.W, tx = row - ty * a.W;
-        m[it] = (ty < a.th && oy0 + ty < a.H) ? ((img * a.H + oy0 + ty) * a.W + tx) : -1;
-        const int mm = m[it] < 0 ? 0 : m[it];  // skipped rows load row 0 (always valid)
-        if (a.res) {
-          const half8 rv = *reinterpret_cast<const half8*>(a.res + (size_t)mm * 64 + nb8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) yv[it][e] = static_cast<float>(rv[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) yv[it][e] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < ITEMS; ++it) {
-        const int row = r0 + it * RSTEP;
-        const float* src = T + row * BN + (nb8 ^ (((row >> 2) & 3) << 4));
-        const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
-        const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
-        half8 h;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float v = (e < 4 ? x0[e] : x1[e - 4]) + bv[e] + yv[it][e];
-          if (a.relu) v = v > 0.f ? v : 0.f;
-          h[e] = static_cast<_Float16>(v);
-        }
-        if (m[it] >= 0) *reinterpret_cast<half8*>(a.y + (size_t)m[it] * 64 + nb8) = h;
+      for (int e = 0; e < 8; ++e) {
+        float v = (e < 4 ? x0[e] + b0[e] : x1[e - 4] + b1[e - 4]);
+        if constexpr (HAS_RES) v += static_cast<float>(rv[it][e]);
+        if constexpr (RELU) v = v > 0.f ? v : 0.f;
+        hv[it][e] = static_cast<_Float16>(v);
       }
     }
+#pragma unroll
+    for (int it = 0; it < E_ITEMS; ++it) {
+#if defined(SPI_WRES_DIAG) && SPI_WRES_DIAG == 1  // diagnostic: no output stores (values kept live)
+      asm volatile("" ::"v"(hv[it]));
+#else
+      if (e_ty[it] < rows_left) *reinterpret_cast<half8*>(a.y + (mbase + e_rel[it]) * 64 + e_nb8) = hv[it];
+#endif
+    }
     lds_barrier();  // the tile is read before the next band's halo DMA reuses this buffer
+    if (NBUF == 1 && more) issue_halo(band + 1, 0);
+    if (sk >= 0) WRES_STAMP(sk + 2);
+  };
+
+  issue_halo(b_first, 0);
+  if constexpr (NBUF == 1) {
+    for (int j = 0; j < nb; ++j) band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
+  } else {
+    for (int j = 0; j < nb; j += 2) {
+      band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
+      if (j + 1 < nb) band_body(std::integral_constant<int, 1>{}, b_first + j + 1, j + 2 < nb, j == 0 ? 4 : -1);
+    }
   }
+  WRES_STAMP(7);
+#ifdef SPI_WRES_STAMPS
+  if (tid == 0 && blockIdx.x < 4096) g_wres_stamps[blockIdx.x * 10 + 8] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 int env_int(const char* name, int dflt) {
@@ -225,7 +339,29 @@ int env_int(const char* name, int dflt) {
   return e && *e ? std::atoi(e) : dflt;
 }
 
+// SPI_CONV_WRES=0: never route here; SPI_CONV_WRES_BPW=n: bands per workgroup (0 = rule);
+// SPI_CONV_WRES_NBUF=2: the double-buffered kernel even for one band per workgroup.
+// Read once; conv_wres_reload_env() (spi_debug_gemm_reload_env) re-reads them for sweeps.
+struct WresKnobs {
+  int on = 1, bpw = 0, nbuf = 0;
+};
+WresKnobs read_wres_knobs() {
+  return WresKnobs{env_int("SPI_CONV_WRES", 1), env_int("SPI_CONV_WRES_BPW", 0), env_int("SPI_CONV_WRES_NBUF", 0)};
+}
+WresKnobs& wres_knobs() {
+  static WresKnobs k = read_wres_knobs();
+  return k;
+}
+
 }  // namespace
+
+void conv_wres_reload_env() { wres_knobs() = read_wres_knobs(); }
+
+#ifdef SPI_WRES_STAMPS
+extern "C" int spi_debug_wres_stamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wres_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // Output rows per band: as many as fill the 128-row tile while the halo fits 256 pixels.
 static int wres_rows(int H, int W) {
@@ -235,7 +371,7 @@ static int wres_rows(int H, int W) {
 }
 
 bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p) {
-  static const int on = env_int("SPI_CONV_WRES", 1);
+  const int on = wres_knobs().on;
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   return on && prec == Prec::F16 && d.conv && d.KH == 3 && d.KW == 3 && d.stride == 1 && d.pad == 1 &&
          d.Cin == 64 && d.N == 64 && d.K == 576 && d.Kpad == 576 && d.krep == 1 && d.OH == d.H && d.OW == d.W &&
@@ -248,7 +384,7 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   WresArgs a{};
   a.x = static_cast<const _Float16*>(p.A);
   a.w = static_cast<const char*>(p.W);
-  a.bias = p.bias;
+  a.bias = p.bias ? p.bias : static_cast<const float*>(p.zeros);  // the zero line: 64 floats
   a.res = static_cast<const _Float16*>(p.res);
   a.y = static_cast<_Float16*>(p.C);
   a.zeros = static_cast<const char*>(p.zeros);
@@ -259,14 +395,25 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.bands_per_img = (d.H + a.th - 1) / a.th;
   const int imgs = d.M / (d.OH * d.OW);
   a.bands = imgs * a.bands_per_img;
-  a.relu = d.act == Act::Relu;
+  const bool relu = d.act == Act::Relu;
   // bands per workgroup (SPI_CONV_WRES_BPW): 1 keeps the most workgroups in flight (the weights
   // are re-read from L2 per band), more amortise the 72 KiB weight fill over several bands
-  static const int bpw_env = env_int("SPI_CONV_WRES_BPW", 0);
+  const int bpw_env = wres_knobs().bpw;
   int bpw = bpw_env > 0 ? bpw_env : (a.bands >= 512 ? 2 : 1);
   a.bpw = std::max(1, bpw);
   const int grid = (a.bands + a.bpw - 1) / a.bpw;
-  hipLaunchKernelGGL(conv3x3_c64_wres, dim3(grid), dim3(NT), 0, s, a);
+  // one halo buffer (104 KiB of LDS) unless a workgroup walks several bands
+  // (SPI_CONV_WRES_NBUF=2 forces the double-buffered kernel)
+  const bool two = a.bpw > 1 || wres_knobs().nbuf == 2;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, s, a); };
+  if (a.res && relu)
+    two ? go(conv3x3_c64_wres<true, true, 2>) : go(conv3x3_c64_wres<true, true, 1>);
+  else if (a.res)
+    two ? go(conv3x3_c64_wres<true, false, 2>) : go(conv3x3_c64_wres<true, false, 1>);
+  else if (relu)
+    two ? go(conv3x3_c64_wres<false, true, 2>) : go(conv3x3_c64_wres<false, true, 1>);
+  else
+    two ? go(conv3x3_c64_wres<false, false, 2>) : go(conv3x3_c64_wres<false, false, 1>);
 }
 
 }  // namespace spi

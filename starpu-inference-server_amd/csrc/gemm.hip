@@ -1520,7 +1520,10 @@ size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }
 
-extern "C" void spi_debug_gemm_reload_env(void) { knobs() = read_knobs(); }
+extern "C" void spi_debug_gemm_reload_env(void) {
+  knobs() = read_knobs();
+  conv_wres_reload_env();
+}
 
 #ifdef SPI_GEMM_STAMPS
 extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {

@@ -32,6 +32,21 @@ void pack_matrix_into(char* dst, int N, int K, int Npad, int Kpad, Prec prec, F 
         row[32] = static_cast<_Float16>(v - static_cast<float>(hi));
       }
     }
+  // A 64 x 576 fp16 matrix (a 3x3 conv over 64 channels, k = tap * 64 + c) leaves its 64
+  // padding rows unused by every GEMM tile that can run it (N = 64: one 64-column tile):
+  // they hold the weight-resident conv's LDS image instead (conv_wres.hip) -- per tap t,
+  // row n, 16-byte slot s: chunk s ^ (n & 7) of W[n][t * 64 ...] -- so that kernel fills
+  // its LDS with 72 contiguous 1-KiB pieces.
+  if (prec == Prec::F16 && N == 64 && K == 576 && Npad == 128 && Kpad == 576) {
+    const _Float16* w = reinterpret_cast<const _Float16*>(dst);
+    _Float16* img = reinterpret_cast<_Float16*>(dst) + (size_t)64 * Kpad;
+    for (int t = 0; t < 9; ++t)
+      for (int n = 0; n < 64; ++n)
+        for (int sl = 0; sl < 8; ++sl) {
+          const int c = sl ^ (n & 7);
+          for (int e = 0; e < 8; ++e) img[((size_t)t * 64 + n) * 64 + sl * 8 + e] = w[(size_t)n * Kpad + t * 64 + c * 8 + e];
+        }
+  }
 }
 
 }  // namespace spi

@@ -898,6 +898,46 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       if (!wok) return cleanup_fail("stream creation failed for worker " + std::to_string(wid - 1));
     }
   }
+  // Every slot's transfer path exercised once before serving: the first SDMA copy from a
+  // pinned buffer (or the first copy on a stream) costs far more than the steady state --
+  // the first measured requests of a fresh runtime had shown 10-19 ms latencies beside a
+  // 3 ms p50 (tools/e2e_tail.py) -- so the copy engines, queues and mappings are set up now.
+  for (size_t dv = 0; dv < rt->pools.size(); ++dv) {
+    SlotPool& pl = *rt->pools[dv];
+    (void)hipSetDevice(pl.device);
+    Worker* w0 = nullptr;
+    for (auto& w : rt->workers)
+      if (w->pool == (int)dv) {
+        w0 = w.get();
+        break;
+      }
+    hipStream_t st = pl.copy_stream ? pl.copy_stream : w0->stream;
+    for (Slot& sl : pl.slots) {
+      for (size_t i = 0; i < sl.h_in.size(); ++i) {
+        const size_t bytes = rt->in_sample_bytes[i] * (size_t)cfg.max_batch;
+        std::memset(sl.h_in[i], 0, bytes);
+        if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
+          hsa_signal_store_screlease(w0->h2d_signal, 1);
+          if (hsa_amd_memory_async_copy(sl.d_in[i], pl.gpu_agent, sl.h_in[i], pl.cpu_agent, bytes, 0, nullptr,
+                                        w0->h2d_signal) != HSA_STATUS_SUCCESS)
+            return cleanup_fail("SDMA warm-up copy failed on device " + std::to_string(pl.device));
+          hsa_signal_value_t v = hsa_signal_load_scacquire(w0->h2d_signal);
+          while (v >= 1)
+            v = hsa_signal_wait_scacquire(w0->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                          HSA_WAIT_STATE_ACTIVE);
+          if (v < 0) return cleanup_fail("SDMA warm-up copy failed on device " + std::to_string(pl.device));
+        } else if (hipMemcpyAsync(sl.d_in[i], sl.h_in[i], bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+          return cleanup_fail("H2D warm-up copy failed on device " + std::to_string(pl.device));
+        }
+      }
+      for (size_t i = 0; i < sl.h_out.size(); ++i)
+        if (hipMemcpyAsync(sl.h_out[i], sl.d_out[i], rt->out_sample_bytes[i] * (size_t)cfg.max_batch,
+                           hipMemcpyDeviceToHost, w0->stream) != hipSuccess)
+          return cleanup_fail("D2H warm-up copy failed on device " + std::to_string(pl.device));
+    }
+    if (hipStreamSynchronize(st) != hipSuccess || hipStreamSynchronize(w0->stream) != hipSuccess)
+      return cleanup_fail("transfer warm-up failed on device " + std::to_string(pl.device));
+  }
   // Per-worker warm-up before serving (the reference warms every worker through the
   // pipeline, inference_runner.cpp:507-560): the workspace and the graph of every batch
   // size the batchers can compose, so no capture (serialised process-wide) or workspace

@@ -62,7 +62,7 @@ struct GemmPtrs {
   void* C = nullptr;
   float* partial = nullptr;  // split-K slabs (gemm_partial_floats)
   int* counters = nullptr;   // split-K arrival tickets, zero-initialised (gemm_counter_slots)
-  const void* zeros = nullptr;  // >= 16 zero bytes (source of padded / out-of-range chunks)
+  const void* zeros = nullptr;  // >= 256 zero bytes (padded / out-of-range chunks; conv_wres: a null bias)
 };
 
 // Workspace needed by a GEMM with the chosen split-K (0 when not split).
@@ -89,6 +89,7 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
 // routes an eligible desc to it (SPI_CONV_WRES=0: never).
 bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p);
 void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
+void conv_wres_reload_env();
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,

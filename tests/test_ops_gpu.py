@@ -376,15 +376,16 @@ def test_gemm256_unaligned_output(ops, gemm256_everywhere):
 
 
 @pytest.mark.parametrize("B,H", [(8, 56), (1, 56), (3, 16), (2, 13), (2, 40), (5, 28), (1, 61)])
-@pytest.mark.parametrize("res,act", [(True, "relu"), (False, "relu"), (True, None)])
-def test_conv3x3_c64_weight_resident(ops, B, H, res, act):
+@pytest.mark.parametrize("res,act,bias", [(True, "relu", True), (False, "relu", True), (True, None, True),
+                                          (False, None, False)])
+def test_conv3x3_c64_weight_resident(ops, B, H, res, act, bias):
     """The weight-resident 64 -> 64 3x3 conv (conv_wres.hip, ResNet layer 1): bands of 2 rows at
     56 wide, 8 at 16 wide, partial last bands (13, 61), with / without the residual and ReLU,
     against an fp32 conv of the fp16-rounded operands."""
     g = torch.Generator().manual_seed(B * 100 + H)
     x = torch.rand(B, H, H, 64, generator=g).half()
     w = torch.randn(64, 64, 3, 3, generator=g) * (2.0 / 576) ** 0.5
-    b = torch.randn(64, generator=g)
+    b = torch.randn(64, generator=g) if bias else None
     r = torch.randn(B, H, H, 64, generator=g).half() if res else None
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.half().float(), b, 1, 1).permute(0, 2, 3, 1)
     if res:
@@ -392,6 +393,7 @@ def test_conv3x3_c64_weight_resident(ops, B, H, res, act):
     if act == "relu":
         ref = F.relu(ref)
     wp = ops.pack_weight("fp16", ops.conv_weight_matrix(w, 64))
-    out = ops.conv2d("fp16", x.cuda(), wp, 64, 3, 3, 1, 1, bias=b.cuda(), residual=r.cuda() if res else None, act=act)
+    out = ops.conv2d("fp16", x.cuda(), wp, 64, 3, 3, 1, 1, bias=b.cuda() if bias else None,
+                     residual=r.cuda() if res else None, act=act)
     err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
     assert err < 2e-3, f"wres conv B{B} H{H} res={res} act={act}: {err:.3e}"

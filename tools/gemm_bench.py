@@ -67,16 +67,28 @@ def main():
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--halo-cfgs", default="", help="';'-separated SPI_GEMM_HALO_CFG values to sweep ('' = the chooser)")
     ap.add_argument("--batch", type=int, default=0, help="override the conv batch (ResNet-152 bs32: 32)")
+    ap.add_argument("--envs", default="", help="';'-separated knob sets KEY=VAL[&KEY=VAL] to sweep "
+                                               "(e.g. 'SPI_CONV_WRES=0;SPI_CONV_WRES_BPW=2')")
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
     plans = a.plans.split(";") if a.plans else [""]
     if a.halo_cfgs:
         plans = [("halo", c) for c in a.halo_cfgs.split(";")]
+    if a.envs:
+        plans = [("env", c) for c in a.envs.split(";")]
 
     def sweep(fn, label, fl):
         for plan in plans:
-            if isinstance(plan, tuple):
+            if isinstance(plan, tuple) and plan[0] == "env":
+                for other in plans:  # knobs of the other sets: back to their defaults
+                    for kv in filter(None, other[1].split("&")):
+                        os.environ.pop(kv.partition("=")[0], None)
+                for kv in filter(None, plan[1].split("&")):
+                    k, _, v = kv.partition("=")
+                    os.environ[k] = v
+                plan = plan[1] or "default"
+            elif isinstance(plan, tuple):
                 os.environ["SPI_GEMM_HALO_CFG"] = plan[1]
                 plan = "halo " + plan[1]
             else:
@@ -90,6 +102,8 @@ def main():
             print(f"{label}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s  [{plan or 'auto'}]", flush=True)
         os.environ["SPI_GEMM_PLAN"] = ""
         os.environ["SPI_GEMM_HALO_CFG"] = ""
+        for k in ("SPI_CONV_WRES", "SPI_CONV_WRES_BPW"):
+            os.environ.pop(k, None)
         ops.lib.spi_debug_gemm_reload_env()
     dt = ops.act_dtype(a.prec)
     ws = ops.workspace()
