@@ -107,6 +107,14 @@ __device__ unsigned long long g_wres_stamps[4096 * 10];
   } while (0)
 #endif
 
+template <int T, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (T < N) {
+    f(std::integral_constant<int, T>{});
+    static_for<T + 1, N>(f);
+  }
+}
+
 // LDS map: halo buffers at 0 and kHBuf (A fragment reads then use an immediate
 // offset per buffer), the resident weights from 2 * kHBuf.
 
@@ -126,13 +134,18 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   WRES_STAMP(0);
 
   // ---- resident weights: the packed matrix's padding rows hold the LDS image (pack.hpp:
-  // pack_matrix_into), 72 contiguous pieces of 1 KiB, 18 per wave
+  // pack_matrix_into), 72 contiguous pieces of 1 KiB, 18 per wave.  One-band workgroups
+  // (NBUF 1) issue them after the band's halo, two pieces per tap per wave in tap order, and
+  // start each tap as soon as its pieces have landed; the others issue them first.
   const char* wimg = a.w + (size_t)64 * (9 * kRowB);
+  auto issue_w = [&] {
 #pragma unroll
-  for (int i = 0; i < kWPieces; ++i) {
-    const int q = wave * kWPieces + i;
-    glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
-  }
+    for (int i = 0; i < kWPieces; ++i) {
+      const int q = NBUF == 1 ? i * 4 + wave : wave * kWPieces + i;
+      glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
+    }
+  };
+  if constexpr (NBUF == 2) issue_w();
 
   // ---- halo bookkeeping, band-independent: piece i of this wave fills pixels
   // p = (wave * 8 + i) * 8 + lane / 8, slot lane % 8 <- chunk slot ^ (p & 7)
@@ -209,13 +222,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   // flight behind chunk t's eight MFMAs (sched_barrier pins the order; the compiler's
   // counted lgkmcnt then waits only for chunk t).
   auto band_body = [&](auto buf_c, int band, bool next, int sk) {
-    const bool more = next;
     constexpr int BUF = decltype(buf_c)::value;
     // the next band's halo into the buffer band - 1 used (its epilogue ended in a barrier); one
     // buffer: only after this band's epilogue
     if (NBUF == 2 && next) issue_halo(band + 1, BUF ^ 1);
-    if (NBUF == 1) next = false;
-    if (next)
+    if (NBUF == 1)
+      dma_wait_barrier<2 * 8>();  // the halo and tap 0 have landed (taps 1..8 still in flight)
+    else if (next)
       dma_wait_barrier<kHPieces>();  // everything but the next halo has landed
     else
       dma_wait_barrier<0>();
@@ -237,9 +250,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
         fb[s][jj] = *reinterpret_cast<const half8*>(lds + boff[kk][jj] + tap * kWImg);
     };
     load(0, 0);
-#pragma unroll
-    for (int t = 0; t < 18; ++t) {
-      if (t + 1 < 18) load(t + 1, (t + 1) & 1);
+    static_for<0, 18>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (t + 1 < 18) {
+        // one-band workgroups: tap (t + 1) / 2's weight pieces land while taps before it compute
+        if constexpr (NBUF == 1 && (t + 1) % 2 == 0) dma_wait_barrier<2 * (8 - (t + 1) / 2)>();
+        load(t + 1, (t + 1) & 1);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -247,7 +264,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
         for (int jj = 0; jj < 2; ++jj)
           acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t & 1][i], fb[t & 1][jj], acc[i][jj], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-    }
+    });
     if (sk >= 0) WRES_STAMP(sk + 1);
 
     // ---- epilogue through this band's halo buffer (every wave is done reading it).  The
@@ -315,13 +332,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
 #endif
     }
     lds_barrier();  // the tile is read before the next band's halo DMA reuses this buffer
-    if (NBUF == 1 && more) issue_halo(band + 1, 0);
     if (sk >= 0) WRES_STAMP(sk + 2);
   };
 
   issue_halo(b_first, 0);
-  if constexpr (NBUF == 1) {
-    for (int j = 0; j < nb; ++j) band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
+  if constexpr (NBUF == 1) {  // one band per workgroup
+    issue_w();
+    band_body(std::integral_constant<int, 0>{}, b_first, false, 1);
   } else {
     for (int j = 0; j < nb; j += 2) {
       band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
@@ -402,8 +419,8 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   int bpw = bpw_env > 0 ? bpw_env : (a.bands >= 512 ? 2 : 1);
   a.bpw = std::max(1, bpw);
   const int grid = (a.bands + a.bpw - 1) / a.bpw;
-  // one halo buffer (104 KiB of LDS) unless a workgroup walks several bands
-  // (SPI_CONV_WRES_NBUF=2 forces the double-buffered kernel)
+  // one band per workgroup: one halo buffer (104 KiB of LDS); several bands: the
+  // double-buffered kernel (SPI_CONV_WRES_NBUF=2 forces it for one band too)
   const bool two = a.bpw > 1 || wres_knobs().nbuf == 2;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, s, a); };
   if (a.res && relu)
