@@ -132,7 +132,7 @@ enum spi_h2d_mode {
   SPI_H2D_DEVICE_STREAM = 0, /* one copy stream per device, event-joined */
   SPI_H2D_WORKER_STREAM = 1, /* H2D on the worker's own stream */
   SPI_H2D_WORKER_COPY = 2,   /* one copy stream per worker, event-joined */
-  SPI_H2D_AUTO = 3,          /* default: WORKER_SDMA when the task input is >= 64 KiB per GFLOP of the
+  SPI_H2D_AUTO = 3,          /* default: WORKER_SDMA when the task input is >= 120 KiB per GFLOP of the
                                 forward (link-bound serving); otherwise (or without HSA agents)
                                 DEVICE_STREAM for <= 3 workers per device, else WORKER_STREAM */
   SPI_H2D_WORKER_SDMA = 4    /* H2D on an SDMA engine (hsa_amd_memory_async_copy), waited by the worker

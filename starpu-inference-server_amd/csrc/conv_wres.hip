@@ -123,7 +123,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   constexpr int kW0 = NBUF * kHBuf;
   __shared__ __attribute__((aligned(16))) char lds[kLds<NBUF>];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b_first = blockIdx.x * a.bpw;
+  // XCD-aware band order: the hardware deals consecutive workgroups round-robin to the 8
+  // XCDs; remapped, each XCD walks a contiguous run of bands, so the two input rows that
+  // neighbouring bands share are fetched into one L2 once (bijective remap,
+  // cdna_hip_programming.md T1)
+  int wg = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = wg & 7, l = wg >> 3;
+    if (nwg >= 16) wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+  }
+  const int b_first = wg * a.bpw;
   const int nb = min(a.bpw, a.bands - b_first);
   if (nb <= 0) return;  // uniform per workgroup
   const int Wp = a.W + 2;

@@ -220,6 +220,7 @@ struct SlotPool {
   std::condition_variable cv;
   hipStream_t copy_stream = nullptr;  // SPI_H2D_DEVICE_STREAM
   hsa_agent_t gpu_agent{}, cpu_agent{};  // SPI_H2D_WORKER_SDMA
+  uint32_t sdma_engine = 0;              // 0: ROCr assigns the engine; else the hsa_amd_sdma_engine_id_t bit
 
   int acquire() {
     std::unique_lock<std::mutex> lk(mu);
@@ -359,6 +360,15 @@ bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
   return it->second.ok;
 }
 
+// One host -> device SDMA copy: on the pool's pinned engine when one was chosen
+// (SPI_H2D_SDMA_ENGINE), else on the engine ROCr assigns.
+hsa_status_t sdma_h2d(const SlotPool& pl, void* dst, const void* src, size_t bytes, hsa_signal_t sig) {
+  if (pl.sdma_engine)
+    return hsa_amd_memory_async_copy_on_engine(dst, pl.gpu_agent, src, pl.cpu_agent, bytes, 0, nullptr, sig,
+                                               (hsa_amd_sdma_engine_id_t)pl.sdma_engine, true);
+  return hsa_amd_memory_async_copy(dst, pl.gpu_agent, src, pl.cpu_agent, bytes, 0, nullptr, sig);
+}
+
 }  // namespace
 
 struct spi_runtime {
@@ -495,8 +505,8 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
     const SlotPool& pl = *pools[w->pool];
     hsa_signal_store_screlease(w->h2d_signal, ni);
     for (int i = 0; i < ni; ++i)
-      if (hsa_amd_memory_async_copy(slot.d_in[i], pl.gpu_agent, slot.h_in[i], pl.cpu_agent,
-                                    (size_t)t.total * in_sample_bytes[i], 0, nullptr, w->h2d_signal) != HSA_STATUS_SUCCESS) {
+      if (sdma_h2d(pl, slot.d_in[i], slot.h_in[i], (size_t)t.total * in_sample_bytes[i], w->h2d_signal) !=
+          HSA_STATUS_SUCCESS) {
         t.status = SPI_ERR_DEVICE;
         t.err = "SDMA H2D copy failed";
         hsa_signal_subtract_screlease(w->h2d_signal, ni - i);
@@ -808,16 +818,21 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     rt->out_sample_bytes.push_back(es * (size_t)c->output_elems[i]);
   }
   if (cfg.h2d_mode == SPI_H2D_AUTO) {
-    // SDMA-engine copies when the task's input would keep the PCIe link busy: at least
-    // 64 KiB per GFLOP of the forward (at the ~350 TFLOP/s the ResNet-18 headline sustains
-    // a GFLOP is ~3 us, 64 KiB over the 51 GB/s link ~1.3 us) -- ResNet-18 (166 KiB/GFLOP):
-    // e2e 64-68k -> 81-85k inf/s; ResNet-152 (26), ViT-L (5), BERT (0.1) are compute-bound
-    // and measured 5-10 % better on the stream copies.  Those: a shared copy
-    // stream for <= 3 workers, the worker streams beyond (four busy streams per device)
+    // SDMA-engine copies when the task's input keeps the PCIe link busy: at least 120 KiB of
+    // input per GFLOP of the forward.  The threshold sits on a measured crossover
+    // (tools/sdma_crossover.py, bs8, 4 workers, 32 in flight, profiles/r03/sdma_crossover.log):
+    // SDMA / stream e2e = 1.116 for ResNet-18 (162 KiB/GFLOP), 0.952 ResNet-34 (80), 0.930
+    // ResNet-50 (72), 0.949 ResNet-101 (38), 0.950 ResNet-152 (26); ViT-L (5) and BERT (0.1)
+    // lose too.  The compute-bound side loses because the device's kernels run slower beside
+    // the SDMA traffic, not because the worker waits for the copy: pinning the copies to a
+    // free engine (SPI_H2D_SDMA_ENGINE=high) cut ResNet-152's per-task copy wait from ~7 ms to
+    // ~1 ms and the rate still fell (9.2k vs 10.6k inf/s on the streams, tools/sdma_ab.py).
+    // Below the threshold: a shared copy stream for <= 3 workers, the worker streams beyond
+    // (four busy streams per device)
     size_t task_in = 0;
     for (size_t b : rt->in_sample_bytes) task_in += b * (size_t)cfg.max_batch;
     const double gflop = c->models[0] ? spi_model_flops(c->models[0], cfg.max_batch) * 1e-9 : 0.0;
-    bool sdma = gflop > 0.0 && (double)task_in / gflop >= 64.0 * 1024.0;
+    bool sdma = gflop > 0.0 && (double)task_in / gflop >= 120.0 * 1024.0;
     for (int dv = 0; dv < c->num_devices && sdma; ++dv) {
       hsa_agent_t g{}, h{};
       sdma = find_hsa_agents(c->device_ids[dv], g, h);
@@ -877,6 +892,23 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       rt->pools.push_back(std::move(pool));
       return cleanup_fail("no HSA agents for device " + std::to_string(c->device_ids[dv]));
     }
+    if (ok && cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
+      // SPI_H2D_SDMA_ENGINE: "high" = the highest engine free for host -> device copies, N =
+      // engine N, unset = ROCr's choice (shared with HIP's own copies)
+      if (const char* e = std::getenv("SPI_H2D_SDMA_ENGINE"); e && *e) {
+        uint32_t mask = 0;
+        if (hsa_amd_memory_copy_engine_status(pool->gpu_agent, pool->cpu_agent, &mask) == HSA_STATUS_SUCCESS && mask) {
+          if (std::strcmp(e, "high") == 0) {
+            pool->sdma_engine = 1u << (31 - __builtin_clz(mask));
+          } else {
+            const int n = std::atoi(e);
+            if (n >= 0 && n < 16 && (mask >> n) & 1u) pool->sdma_engine = 1u << n;
+          }
+        }
+        std::fprintf(stderr, "spi_runtime: device %d H2D SDMA engines free 0x%x, using 0x%x\n", pool->device, mask,
+                     pool->sdma_engine);
+      }
+    }
     rt->pools.push_back(std::move(pool));
     if (!ok) return cleanup_fail("slot pool allocation failed on device " + std::to_string(c->device_ids[dv]));
     for (int k = 0; k < cfg.workers_per_device; ++k) {
@@ -918,8 +950,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
         std::memset(sl.h_in[i], 0, bytes);
         if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
           hsa_signal_store_screlease(w0->h2d_signal, 1);
-          if (hsa_amd_memory_async_copy(sl.d_in[i], pl.gpu_agent, sl.h_in[i], pl.cpu_agent, bytes, 0, nullptr,
-                                        w0->h2d_signal) != HSA_STATUS_SUCCESS)
+          if (sdma_h2d(pl, sl.d_in[i], sl.h_in[i], bytes, w0->h2d_signal) != HSA_STATUS_SUCCESS)
             return cleanup_fail("SDMA warm-up copy failed on device " + std::to_string(pl.device));
           hsa_signal_value_t v = hsa_signal_load_scacquire(w0->h2d_signal);
           while (v >= 1)
