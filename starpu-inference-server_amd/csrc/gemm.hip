@@ -26,6 +26,7 @@
 // write-through (sc1) and the last to arrive (relaxed agent-scope ticket) sums
 // them with sc1 loads and runs the epilogue -- no second launch, no cache-wide
 // fences (cdna_hip_programming.md, "In-launch split-K reduction").
+#include "device_math.hpp"
 #include "spi_kernels.hpp"
 
 #include <algorithm>
@@ -176,7 +177,7 @@ __device__ __forceinline__ size_t split_idx(int m, int n, int ld) {
 
 __device__ __forceinline__ float apply_act(float v, Act act) {
   if (act == Act::Relu) return v > 0.f ? v : 0.f;
-  if (act == Act::Gelu) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  if (act == Act::Gelu) return gelu(v);
   return v;
 }
 
@@ -1523,6 +1524,7 @@ int gemm_kstep(Prec prec) { return estep_of(prec); }
 extern "C" void spi_debug_gemm_reload_env(void) {
   knobs() = read_knobs();
   conv_wres_reload_env();
+  gemm256_reload_env();
 }
 
 #ifdef SPI_GEMM_STAMPS

@@ -25,10 +25,12 @@
 // barriers after its last read.  LDS images are the general kernel's: 128-byte
 // rows, 16-byte chunk c of row r at slot c ^ (r & 7), swizzle applied on the
 // DMA source address (rule 21), conflict-free ds_read_b128 fragment reads.
+#include "device_math.hpp"
 #include "spi_kernels.hpp"
 
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 namespace spi {
 namespace {
@@ -49,7 +51,6 @@ struct G256Args {
   int act;  // Act
   int res_f32, out_f32;
   int vec_ok;  // C / residual rows and pointers allow 16-byte vectors (LDS-staged epilogue)
-  int diag;  // diagnostic (SPI_G256_DIAG): 1 every k-tile re-reads k-tile 0 (L2-resident), 2 no DMA after the prologue
 };
 
 constexpr int kBufBytes = 65536;  // one k-tile: A 256 x 128 B + B 256 x 128 B
@@ -65,7 +66,41 @@ __device__ __forceinline__ int quarter_row(int q, int pc) {
   }
 }
 
-template <bool AHEAD>
+// RES: 0 no residual, 1 fp16 residual, 2 fp32 residual (a template parameter: the epilogue walk
+// stays branch-free).
+// wait until at most N of this wave's LDS-DMA instructions are outstanding and its LDS
+// reads are done, then a workgroup barrier
+// (the s_waitcnt builtin, not inline asm: hipcc's waitcnt pass then knows the fragment
+// reads are done and does not add an lgkmcnt(0) in front of the next MFMAs, which would
+// wait for the reads issued after this barrier too)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));  // vmcnt(N) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// wait until at most N of this wave's LDS-DMA instructions are outstanding (LDS reads
+// stay in flight), then a workgroup barrier
+template <int N>
+__device__ __forceinline__ void vm_wait_nolgkm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));  // vmcnt(N) only
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// PIPE 1: ping-pong wave rows (default); 0: both wave rows in lock step, two-tile-ahead DMA
+template <int PIPE, int RES>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -103,8 +138,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   }
   auto stage = [&](int q, int kt) {
     char* buf = lds + (kt & 1) * kBufBytes;
-    if (g.diag == 2 && kt > 0) return;
-    const int kofs = g.diag == 1 ? 0 : kt * 128;
+    const int kofs = kt * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[q][j] + kofs),
@@ -147,80 +181,116 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // prologue: k-tile 0 into buffer 0
+  if constexpr (PIPE == 1) {
+    // Ping-pong (cdna_hip_programming.md §5, the 256² 8-phase template): every phase is
+    //   [reads of its fragments, one quarter's LDS-DMA, counted vmcnt] B_a [MFMAs] B_b
+    // and wave row 1 runs one barrier behind wave row 0 (an extra s_barrier up front, one
+    // at the end for row 0), so between any two barriers one wave of each SIMD issues MFMAs
+    // while the other one reads LDS / issues DMA: the MFMA pipe never waits for a read.
+    // Reads: phase 0 A_m0 + B_n0 (Q0, Q1), 1 B_n1 (Q2), 2 A_m1 (Q3), 3 none.  Quarters
+    // go out in one sequence s = 4 k + q, quarter s in global phase s - 6 (Q2 / Q3 of tile
+    // t + 1 in phases 0 / 1 of tile t, Q0 / Q1 of tile t + 2 in phases 2 / 3): a region is
+    // restaged >= 2 phases after its last read (WAR with the one-barrier skew), and a
+    // quarter has ~4 phases to land.  The wait for phase P's quarter sits before B_a of
+    // phase P - 1, so both wave rows have retired it a barrier before either reads it.
+    // vmcnt after this phase's DMA, tile t with R = min(KT - 1 - t, 2) tiles after it:
+    //   phase 0: R >= 1 8, R = 0 2;  phase 1: 8 / 0;  phase 3: R = 2 8, R = 1 4, R = 0 -.
 #pragma unroll
-  for (int q = 0; q < 4; ++q) stage(q, 0);
-
-  if constexpr (AHEAD) {
-    // Fragment reads one phase ahead of their MFMAs: phase p's barrier retires the
-    // quarter the NEXT phase's fragments come from, its reads go out, then its own
-    // MFMAs run on registers read a phase earlier, so LDS latency hides behind
-    // MFMAs.  Reads: phase 0 B_n1(t) [Q2], phase 1 A_m1(t) [Q3], phase 3 A_m0, B_n0
-    // of t + 1 [Q0, Q1]; phase p still stages Q_p(t + 1).  Each quarter is in flight
-    // two phases or more; every wait is vmcnt(2) (last tile: 2, 0).
-    asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    for (int q = 0; q < 6; ++q)
+      if (q < 4 * KT) stage(q & 3, q >> 2);
+    if (KT > 1)
+      vm_wait_nolgkm<8>();
+    else
+      vm_wait_nolgkm<4>();
+    if (wr == 1) bar();  // the skew
+    auto ktile = [&](int kt, auto rem_c) {
+      constexpr int R = decltype(rem_c)::value;
+      const char* buf = lds + (kt & 1) * kBufBytes;
+      // phase 0
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if constexpr (R >= 1) stage(2, kt + 1);
+      vm_wait_nolgkm<R >= 1 ? 8 : 2>();
+      mma(0, 0);
+      bar();
+      // phase 1
+      read_b(buf, 1);
+      if constexpr (R >= 1) stage(3, kt + 1);
+      vm_wait_nolgkm<R >= 1 ? 8 : 0>();
+      mma(0, 1);
+      bar();
+      // phase 2
+      read_a(buf, 1);
+      if constexpr (R >= 2) stage(0, kt + 2);
+      bar();
+      mma(1, 0);
+      bar();
+      // phase 3
+      if constexpr (R >= 2) stage(1, kt + 2);
+      if constexpr (R >= 1)
+        vm_wait_nolgkm<R >= 2 ? 8 : 4>();
+      else
+        bar();
+      mma(1, 1);
+      bar();
+    };
+    for (int kt = 0; kt < KT - 2; ++kt) ktile(kt, std::integral_constant<int, 2>{});
+    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
+    ktile(KT - 1, std::integral_constant<int, 0>{});
+    if (wr == 0) bar();  // the skew, closed
+  } else {
+    // Two-tile-ahead staging.  Every k-tile's quarters go out in two groups, Q01 = {Q0, Q1}
+    // and Q23 = {Q2, Q3} (4 DMA instructions per wave each), and tile t + 2's groups are
+    // issued during tile t: Q01(t + 2) at barrier B0(t), once tile t's Q0 / Q1 fragments
+    // (read a phase ahead, at B3(t - 1)) are in registers, and Q23(t + 2) at B3(t), once
+    // Q2(t) / Q3(t) are.  The one-quarter-ahead schedule this replaces kept 16-32 KiB per
+    // CU in flight and gave a quarter two phases to land; at the loaded L2 / MALL latency
+    // (~1 us) that capped the CU at ~14 B/clk of ingest, 2 us per k-tile against the
+    // 0.85 us of MFMAs (Little's law).  Now up to 96 KiB per CU is in flight and a group
+    // has 1.25-1.75 k-tiles to arrive.  The issue order is one sequence Q01(0) Q23(0)
+    // Q01(1) Q23(1) Q01(2) ..., so each wait counts the instructions issued after the
+    // group it needs (vmcnt; see the table in vm_wait); the lgkmcnt(0) in each wait makes
+    // the previous readers of a region done before any wave restages it (WAR).
+    auto stage2 = [&](int g01, int kt) {  // group g01 (0: Q0+Q1, 1: Q2+Q3) of k-tile kt
+      stage(2 * g01, kt);
+      stage(2 * g01 + 1, kt);
+    };
+    stage2(0, 0);
+    stage2(1, 0);
+    if (KT > 1) {
+      stage2(0, 1);
+      stage2(1, 1);
+      vm_wait<12>();
+    } else {
+      vm_wait<4>();
+    }
     read_a(lds, 0);
     read_b(lds, 0);
-    auto ktile = [&](int kt, auto last_c) {
-      constexpr bool LAST = decltype(last_c)::value;
+    // tile t with R = KT - 1 - t tiles after it (R capped at 2): waits before B0 / B1 / B3
+    //   R >= 2: 10 / 12 / 8,  R = 1: 10 / 8 / 4,  R = 0: 2 / 0 / -
+    auto ktile = [&](int kt, auto rem_c) {
+      constexpr int R = decltype(rem_c)::value;
       const char* buf = lds + (kt & 1) * kBufBytes;
-      asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      vm_wait<R >= 1 ? 10 : 2>();  // B0: Q2(t) landed
       read_b(buf, 1);
-      if constexpr (!LAST) stage(0, kt + 1);
+      if constexpr (R >= 2) stage2(0, kt + 2);
       mma(0, 0);
-      if constexpr (LAST)
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      vm_wait<R >= 2 ? 12 : R == 1 ? 8 : 0>();  // B1: Q3(t) landed
       read_a(buf, 1);
-      if constexpr (!LAST) stage(1, kt + 1);
       mma(0, 1);
-      if constexpr (!LAST) stage(2, kt + 1);
       mma(1, 0);
-      if constexpr (!LAST) {
-        asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      if constexpr (R >= 1) {
+        vm_wait<R >= 2 ? 8 : 4>();  // B3: Q0(t + 1), Q1(t + 1) landed
         const char* nbuf = lds + ((kt + 1) & 1) * kBufBytes;
         read_a(nbuf, 0);
         read_b(nbuf, 0);
-        stage(3, kt + 1);
+        if constexpr (R >= 2) stage2(1, kt + 2);
       }
       mma(1, 1);
     };
-    for (int kt = 0; kt < KT - 1; ++kt) ktile(kt, std::false_type{});
-    ktile(KT - 1, std::true_type{});
-  } else {
-    // one k-tile; the vmcnt before phases 0 / 1 / 2: 4, 4, 4 (the last tile 4, 2, 0)
-    auto ktile = [&](int kt, auto last_c) {
-      constexpr bool LAST = decltype(last_c)::value;
-      const char* buf = lds + (kt & 1) * kBufBytes;
-      // phase 0: quadrant (0, 0)
-      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      read_a(buf, 0);
-      read_b(buf, 0);
-      if constexpr (!LAST) stage(0, kt + 1);
-      mma(0, 0);
-      // phase 1: quadrant (0, 1)
-      if constexpr (LAST)
-        asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      read_b(buf, 1);
-      if constexpr (!LAST) stage(1, kt + 1);
-      mma(0, 1);
-      // phase 2: quadrant (1, 0)
-      if constexpr (LAST)
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      read_a(buf, 1);
-      if constexpr (!LAST) stage(2, kt + 1);
-      mma(1, 0);
-      // phase 3: quadrant (1, 1) from registers
-      if constexpr (!LAST) stage(3, kt + 1);
-      mma(1, 1);
-    };
-    for (int kt = 0; kt < KT - 1; ++kt) ktile(kt, std::false_type{});
-    ktile(KT - 1, std::true_type{});
+    for (int kt = 0; kt < KT - 2; ++kt) ktile(kt, std::integral_constant<int, 2>{});
+    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
+    ktile(KT - 1, std::integral_constant<int, 0>{});
   }
 
   // Epilogue through LDS (the k-loop's buffers are free): per-element stores from the
@@ -234,7 +304,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   const Act act = static_cast<Act>(g.act);
   auto finish = [&](float y) {
     if (act == Act::Relu) return y > 0.f ? y : 0.f;
-    if (act == Act::Gelu) return 0.5f * y * (1.f + erff(y * 0.70710678118654752f));
+    if (act == Act::Gelu) return gelu(y);
     return y;
   };
   if (!g.vec_ok) {
@@ -266,75 +336,159 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     return;
   }
+  // The walk is branch-free per row: the residual kind (none / fp16 / fp32) is a template
+  // parameter and rows past M load a clamped, valid row (and store duplicates, below).  A runtime
+  // `if (res)` or a guarded bias load per element had hipcc branch around each load and wait
+  // vmcnt(0) per row (the weight-resident conv measured that as 40 % of its epilogue).  Each
+  // thread's 8 residual rows of a round are loaded before the round's park, so their latency
+  // hides behind it.
   float* T = reinterpret_cast<float*>(lds);
   const int cg = tid & 31, r0 = tid >> 5;  // 8-column group, first row of this thread
   const int nb = n0 + 8 * cg;
   float bias8[8];
+  if (g.bias) {
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(g.bias + nb);
+    const floatx4 b1 = *reinterpret_cast<const floatx4*>(g.bias + nb + 4);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bias8[e] = g.bias ? g.bias[nb + e] : 0.f;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __syncthreads();  // the k-loop's last reads / the previous round's walk are done
-    if (wr == h) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int row = 16 * a + 4 * fq + v;
-            const int col = (64 * wc + 16 * b + fr) ^ (((row >> 2) & 3) << 4);
-            T[row * 256 + col] = acc[a][b][v];
-          }
+    for (int e = 0; e < 4; ++e) {
+      bias8[e] = b0[e];
+      bias8[e + 4] = b1[e];
     }
-    __syncthreads();
-#pragma unroll 2
-    for (int pass = 0; pass < 8; ++pass) {
-      const int row = r0 + 16 * pass;
-      const int m = m0 + 128 * h + row;
-      if (m >= g.M) continue;
-      const float* src = T + row * 256 + ((8 * cg) ^ (((row >> 2) & 3) << 4));
-      const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
-      const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
-      float y[8];
+  } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        y[e] = x0[e] + bias8[e];
-        y[e + 4] = x1[e] + bias8[e + 4];
+    for (int e = 0; e < 8; ++e) bias8[e] = 0.f;
+  }
+  // activation and output format are dispatched once, outside the rounds
+  auto epi = [&](auto act_c, auto f32_c) {
+    constexpr int ACT = decltype(act_c)::value;
+    constexpr bool OUTF32 = decltype(f32_c)::value;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // residual rows: the first half of the round's prefetched, the rest loaded inside the
+      // walk (all eight would spill next to the accumulators the other wave row still holds)
+      constexpr int PRE = 4;
+      half8 rvh[RES == 1 ? PRE : 1];
+      floatx4 rvf[RES == 2 ? PRE : 1][2];
+      auto res_row = [&](int pass) -> size_t {
+        const int m = min(m0 + 128 * h + r0 + 16 * pass, g.M - 1);
+        return (size_t)m * g.ldr + nb;
+      };
+      if constexpr (RES == 1) {
+#pragma unroll
+        for (int pass = 0; pass < PRE; ++pass)
+          rvh[pass] = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) + res_row(pass));
       }
-      if (g.res) {
-        const size_t ri = (size_t)m * g.ldr + nb;
-        if (g.res_f32) {
-          const floatx4 q0 = *reinterpret_cast<const floatx4*>(static_cast<const float*>(g.res) + ri);
-          const floatx4 q1 = *reinterpret_cast<const floatx4*>(static_cast<const float*>(g.res) + ri + 4);
+      if constexpr (RES == 2) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            y[e] += q0[e];
-            y[e + 4] += q1[e];
-          }
-        } else {
-          const half8 q = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) + ri);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] += static_cast<float>(q[e]);
+        for (int pass = 0; pass < PRE; ++pass) {
+          const float* rp = static_cast<const float*>(g.res) + res_row(pass);
+          rvf[pass][0] = *reinterpret_cast<const floatx4*>(rp);
+          rvf[pass][1] = *reinterpret_cast<const floatx4*>(rp + 4);
         }
       }
+      __syncthreads();  // the k-loop's last reads / the previous round's walk are done
+      if (wr == h) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = finish(y[e]);
-      const size_t ci = (size_t)m * g.ldc + nb;
-      if (g.out_f32) {
-        *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci) = floatx4{y[0], y[1], y[2], y[3]};
-        *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci + 4) = floatx4{y[4], y[5], y[6], y[7]};
-      } else {
-        half8 o;
+        for (int a = 0; a < 8; ++a)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = static_cast<_Float16>(y[e]);
-        *reinterpret_cast<half8*>(static_cast<_Float16*>(g.C) + ci) = o;
+          for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int row = 16 * a + 4 * fq + v;
+              const int col = (64 * wc + 16 * b + fr) ^ (((row >> 2) & 3) << 4);
+              T[row * 256 + col] = acc[a][b][v];
+            }
+      }
+      __syncthreads();
+      {
+#pragma unroll
+        for (int pass = 0; pass < 8; ++pass) {
+          const int row = r0 + 16 * pass;
+          const int m = m0 + 128 * h + row;
+          const float* src = T + row * 256 + ((8 * cg) ^ (((row >> 2) & 3) << 4));
+          const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
+          const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
+          float r[8] = {};
+          if constexpr (RES == 1) {
+            const half8 q = pass < PRE ? rvh[pass % PRE]
+                                       : *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) +
+                                                                         res_row(pass));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = static_cast<float>(q[e]);
+          }
+          if constexpr (RES == 2) {
+            floatx4 q0, q1;
+            if (pass < PRE) {
+              q0 = rvf[pass % PRE][0];
+              q1 = rvf[pass % PRE][1];
+            } else {
+              const float* rp = static_cast<const float*>(g.res) + res_row(pass);
+              q0 = *reinterpret_cast<const floatx4*>(rp);
+              q1 = *reinterpret_cast<const floatx4*>(rp + 4);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              r[e] = q0[e];
+              r[e + 4] = q1[e];
+            }
+          }
+          float y[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            y[e] = (e < 4 ? x0[e] : x1[e - 4]) + bias8[e] + r[e];
+            if constexpr (ACT == (int)Act::Relu) y[e] = y[e] > 0.f ? y[e] : 0.f;
+          }
+          if constexpr (ACT == (int)Act::Gelu) {
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const float2v g2 = gelu2(float2v{y[e], y[e + 1]});
+              y[e] = g2.x;
+              y[e + 1] = g2.y;
+            }
+          }
+          // rows past M store to row M - 1: their A rows were loaded clamped to M - 1 (and their
+          // residual rows too), so the values are bit-identical to that row's -- a duplicate
+          // write instead of a branch around each pass's stores
+          const size_t ci = (size_t)min(m, g.M - 1) * g.ldc + nb;
+          if constexpr (OUTF32) {
+            *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci) = floatx4{y[0], y[1], y[2], y[3]};
+            *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci + 4) = floatx4{y[4], y[5], y[6], y[7]};
+          } else {
+            half8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = static_cast<_Float16>(y[e]);
+            *reinterpret_cast<half8*>(static_cast<_Float16*>(g.C) + ci) = o;
+          }
+        }
       }
     }
-  }
+};
+  auto by_act = [&](auto f32_c) {
+    if (act == Act::Gelu)
+      epi(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
+    else if (act == Act::Relu)
+      epi(std::integral_constant<int, (int)Act::Relu>{}, f32_c);
+    else
+      epi(std::integral_constant<int, (int)Act::None>{}, f32_c);
+  };
+  if (g.out_f32)
+    by_act(std::true_type{});
+  else
+    by_act(std::false_type{});
 }
 
 }  // namespace
+
+static int g_pipe = -1;
+static int g256_pipe() {
+  if (g_pipe < 0) {
+    const char* e = std::getenv("SPI_G256_PIPE");  // 1 ping-pong wave rows (default), 0 lock step
+    g_pipe = e && *e ? std::atoi(e) : 1;
+  }
+  return g_pipe;
+}
+
+void gemm256_reload_env() { g_pipe = -1; }
 
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles) {
   if (min_tiles <= 0 || prec != Prec::F16 || d.conv || d.krep != 1 || d.a_split || d.out_split || d.pool_rows ||
@@ -364,21 +518,26 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   g.act = static_cast<int>(d.act);
   g.res_f32 = d.res_f32;
   g.out_f32 = d.out_f32;
-  static const int diag = [] {
-    const char* e = std::getenv("SPI_G256_DIAG");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  g.diag = diag;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  g.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res))) ? 1 : 0;
-  static const int sched = [] {
-    const char* e = std::getenv("SPI_G256_SCHED");  // 1: fragment reads a phase ahead (default), 0: in-phase
-    return e && *e ? std::atoi(e) : 1;
-  }();
-  if (sched)
-    hipLaunchKernelGGL(gemm256_kernel<true>, dim3(g.tiles_m * g.tiles_n), dim3(512), 0, s, g);
-  else
-    hipLaunchKernelGGL(gemm256_kernel<false>, dim3(g.tiles_m * g.tiles_n), dim3(512), 0, s, g);
+  g.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res))) && (!p.bias || al16(p.bias))
+                 ? 1 : 0;
+  const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
+  const dim3 grid(g.tiles_m * g.tiles_n), blk(512);
+  if (g256_pipe() == 1) {
+    if (res == 0)
+      hipLaunchKernelGGL((gemm256_kernel<1, 0>), grid, blk, 0, s, g);
+    else if (res == 1)
+      hipLaunchKernelGGL((gemm256_kernel<1, 1>), grid, blk, 0, s, g);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<1, 2>), grid, blk, 0, s, g);
+  } else {
+    if (res == 0)
+      hipLaunchKernelGGL((gemm256_kernel<0, 0>), grid, blk, 0, s, g);
+    else if (res == 1)
+      hipLaunchKernelGGL((gemm256_kernel<0, 1>), grid, blk, 0, s, g);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<0, 2>), grid, blk, 0, s, g);
+  }
 }
 
 }  // namespace spi

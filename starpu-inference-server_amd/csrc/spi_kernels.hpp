@@ -83,6 +83,7 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 // at least min_tiles 256^2 tiles; SPI_GEMM_256_MIN, default 128, 0 = never).
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
 void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
+void gemm256_reload_env();  // re-read SPI_G256_PIPE
 
 // Weight-resident 3x3/s1/p1 conv, 64 -> 64 channels, fp16 NHWC (conv_wres.hip): the
 // folded weights stay in LDS while a workgroup walks bands of output rows; gemm()

@@ -80,3 +80,19 @@ def test_bench_gpus_2_spawns_two_ranks_control_path():
     e = line["e2e"]
     assert e["requests"] == 200 and abs(e["seconds"] - 0.2) < 1e-9 and e["p50_latency_ms"] == 2.0
     assert abs(e["value"] - 200 * 8 / 0.2) < 1e-6 and len(e["per_rank"]) == 2
+
+
+def test_fast_erf_in_gemm_epilogues_meets_fp32_bar():
+    """The GELU epilogues' erf (csrc/device_math.hpp, coefficients parsed from the header)
+    in fp32 against scipy's erf: max |error| < 5e-7, GELU error / max|x| < 1e-6, so GELU
+    outputs stay inside the fp32 parity bar (1e-5 normalised)."""
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "fast_erf_check.py")
+    spec = importlib.util.spec_from_file_location("fast_erf_check", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    e_erf, e_gelu = mod.max_error(n=400_001)
+    assert e_erf < 5e-7 and e_gelu < 1e-6
+    e16, g16 = mod.max_error(n=400_001, suffix="16")  # gemm256's lower-order form (fp16 operands)
+    assert e16 < 3e-6 and g16 < 2e-6

@@ -66,6 +66,11 @@ def main():
     ap.add_argument("--plans", default="", help="';'-separated SPI_GEMM_PLAN values to sweep ('' = the chooser)")
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--halo-cfgs", default="", help="';'-separated SPI_GEMM_HALO_CFG values to sweep ('' = the chooser)")
+    ap.add_argument("--model-epi", action="store_true",
+                    help="the transformer plans' epilogues: qkv bias->fp16, ff1 bias+GELU->fp16, out/ff2 "
+                         "bias+fp32 residual->fp32 (default: no bias, fp32 out)")
+    ap.add_argument("--kscan", default="", help="MxN: time an f16+bias GEMM of that shape for K = 64 .. 4096")
+    ap.add_argument("--epi-variants", action="store_true", help="with --model-epi: GELU launches also without GELU")
     ap.add_argument("--batch", type=int, default=0, help="override the conv batch (ResNet-152 bs32: 32)")
     ap.add_argument("--envs", default="", help="';'-separated knob sets KEY=VAL[&KEY=VAL] to sweep "
                                                "(e.g. 'SPI_CONV_WRES=0;SPI_CONV_WRES_BPW=2')")
@@ -107,6 +112,17 @@ def main():
         ops.lib.spi_debug_gemm_reload_env()
     dt = ops.act_dtype(a.prec)
     ws = ops.workspace()
+    if a.kscan:  # ViT-L FFN1's M x N over K: the slope is the k-loop, the intercept the fixed cost
+        M, N_ = (int(v) for v in a.kscan.split("x"))
+        rng = np.random.default_rng(0)
+        for K in (64, 128, 256, 512, 1024, 2048, 4096):
+            A = torch.randn(M, K, device="cuda").to(dt)
+            wp = ops.pack_weight(a.prec, rng.standard_normal((N_, K)).astype(np.float32) * 0.05)
+            bias = torch.randn(N_, device="cuda") * 0.1
+            out = torch.empty(M, N_, device="cuda", dtype=dt)
+            sweep(lambda: ops.gemm(a.prec, A, wp, N_, bias=bias, out=out, ws=ws),
+                  f"gemm kscan M={M:6d} N={N_:4d} K={K:5d} f16", 2.0 * M * N_ * K)
+        return
     rng = np.random.default_rng(0)
     for name, B, H, cin, cout, k, st in CONVS:
         if a.only and a.only not in name:
@@ -127,8 +143,20 @@ def main():
         A = torch.randn(M, K, device="cuda").to(dt)
         w = rng.standard_normal((N_, K)).astype(np.float32) * 0.05
         wp = ops.pack_weight(a.prec, w)
-        out = torch.empty(M, N_, device="cuda", dtype=torch.float32)
         fl = 2.0 * M * N_ * K
+        if a.model_epi:
+            bias = torch.randn(N_, device="cuda") * 0.1
+            f16 = "qkv" in name or "ff1" in name
+            act = "gelu" if "ff1" in name else None
+            res = None if f16 else torch.randn(M, N_, device="cuda")
+            out = torch.empty(M, N_, device="cuda", dtype=dt if f16 else torch.float32)
+            sweep(lambda: ops.gemm(a.prec, A, wp, N_, bias=bias, residual=res, out=out, act=act, ws=ws),
+                  f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d} {'gelu ' if act else ''}{'f16' if f16 else 'f32+res'}", fl)
+            if act and a.epi_variants:  # the same launch without the activation: what the GELU costs
+                sweep(lambda: ops.gemm(a.prec, A, wp, N_, bias=bias, out=out, ws=ws),
+                      f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d} f16 (no GELU)", fl)
+            continue
+        out = torch.empty(M, N_, device="cuda", dtype=torch.float32)
         sweep(lambda: ops.gemm(a.prec, A, wp, N_, out=out, ws=ws), f"gemm {name:10s} M={M:6d} N={N_:4d} K={K:5d}", fl)
 
 
