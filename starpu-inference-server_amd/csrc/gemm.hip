@@ -126,6 +126,11 @@ struct KArgs {
   // blocks, h_bps of them per split-K slice
   int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
   int splits;  // split-K slices (the grid holds tiles x splits workgroups of this problem)
+  // split-K grids: workgroups are decoded so that a tile's slices run on one XCD where the
+  // XCD chunking allows it, and those tiles reduce through that XCD's L2 (plain stores and
+  // loads) instead of write-through slabs (SPI_GEMM_SPLIT_LOCAL=1; measured -10 % fetch on
+  // the layer-3 convs, writes unchanged, four-stream ResNet-18 -1.4 %: off by default)
+  int split_local;
 };
 
 // One launch, one or two independent problems of the same kernel instance (a
@@ -267,7 +272,7 @@ constexpr int kMinWaves = std::max(
 // gemm_kernel passes its own arguments (constant kernarg offsets, preloadable);
 // gemm_kernel_pair selects one of two problems at run time.
 template <int MODE, int BM, int BN, int STAGES, int KIND, int NW>
-__device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, const int lin) {
+__device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, const int lin, const int hl) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
@@ -295,8 +300,21 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, cons
   // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
-  int tile = lin;
-  {
+  int tile = lin, kslice = kslice_in;
+  [[maybe_unused]] bool xlocal = false;  // this tile's slices all run on one XCD
+  if (kSplitK<BM, BN, KIND> && a.splits > 1) {
+    // hl: the workgroup's dispatch index inside this problem's range; the hardware deals
+    // dispatch indices round-robin to the 8 XCDs, so hl & 7 names the XCD.  Number each
+    // XCD's workgroups consecutively (bijective, chunks of q or q + 1), then cut that order
+    // into tiles of `splits` consecutive slices: a tile whose slices fall in one chunk is
+    // XCD-local.
+    const int S = a.splits, nwg = a.tiles * S, q = nwg >> 3, r = nwg & 7, x = hl & 7, l = hl >> 3;
+    const int wgid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+    tile = wgid / S;
+    kslice = wgid - tile * S;
+    const auto chunk = [&](int w) { return w < r * (q + 1) ? w / (q + 1) : r + (w - r * (q + 1)) / max(q, 1); };
+    xlocal = a.split_local && chunk(tile * S) == chunk(tile * S + S - 1);
+  } else {
     const int nwg = a.tiles, q = nwg >> 3, r = nwg & 7, x = tile & 7, l = tile >> 3;
     if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
   }
@@ -1038,13 +1056,25 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, cons
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(tile_slabs, (short)0, splits * SLAB * 4, 0x00020000);
+  // XCD-local tiles: plain stores into this XCD's L2 (written back later, never read back
+  // from memory); others: write-through (sc1) so a reducer on another XCD sees them
+  if (xlocal) {
 #pragma unroll
-  for (int i = 0; i < TI; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
-    }
+      for (int j = 0; j < TJ; ++j) {
+        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 0);
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+      }
+  }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (tid == 0) {
     const int ticket = __hip_atomic_fetch_add(a.p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1064,17 +1094,32 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, cons
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // (XCD-local: plain loads from this XCD's L2 -- no L1 line of these slabs can be stale:
+  // the L1 is invalidated at dispatch and only this reducer reads the tile's slabs)
+  const int rd_pol = xlocal ? 0 : 16;
   for (int z0 = 0; z0 < splits; z0 += ZR) {
     floatx4 v[ZR][TI][TJ];
+    if (rd_pol == 0) {
 #pragma unroll
-    for (int zz = 0; zz < ZR; ++zz)
+      for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-          v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-        }
+          for (int j = 0; j < TJ; ++j) {
+            const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+            v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          }
+    } else {
+#pragma unroll
+      for (int zz = 0; zz < ZR; ++zz)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+            v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+          }
+    }
 #pragma unroll
     for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
@@ -1088,7 +1133,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice, cons
 
 template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
 __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel(KArgs a) {
-  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, blockIdx.y, blockIdx.x);
+  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, blockIdx.y, blockIdx.x, blockIdx.x + blockIdx.y * a.tiles);
 }
 
 // Grouped launch (KGroup): 1-D grid, problem-major, then slice, then tile.
@@ -1099,7 +1144,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   if (second) lin -= g.wgs0;
   const KArgs& a = second ? g.a[1] : g.a[0];
   const int kslice = lin / a.tiles;
-  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, kslice, lin - kslice * a.tiles);
+  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, kslice, lin - kslice * a.tiles, lin);
 }
 
 struct Plan {
@@ -1141,6 +1186,7 @@ struct Knobs {
   };
   HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
   int n_halo_map = 0;
+  int split_local = 0;  // SPI_GEMM_SPLIT_LOCAL=1: XCD-local split-K tiles reduce through L2
   int xcd2d = 2;  // 2-D tile -> XCD rectangles (xcd_groups); 2: not for split-K grids (plain order there)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
 
@@ -1163,6 +1209,7 @@ Knobs read_knobs() {
   }
   if (const char* e = std::getenv("SPI_GEMM_HALO"); e && *e) k.halo = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_XCD2D"); e && *e) k.xcd2d = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_SPLIT_LOCAL"); e && *e) k.split_local = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
@@ -1386,6 +1433,7 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   a.p = p;
   a.k_per_split = pl.k_per_split;
   a.splits = pl.splits;
+  a.split_local = knobs().split_local;
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
   xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, a.tiles_m, a.tiles / a.tiles_m, a.xg_m, a.xg_n);
