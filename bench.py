@@ -224,6 +224,16 @@ def committed_profile(kind, model, batch, precision):
         return json.load(f).get("ops", {}), os.path.relpath(hits[-1], ROOT)
 
 
+def committed_rocprof(op):
+    """The newest profiles/<round>/roofline_rocprof.json entry for `op` (tools/rocprof_roofline.py)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "roofline_rocprof.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f).get(op)
+        if rec:
+            return rec
+    return None
+
+
 def roofline(h, precision, model, reps=200, name=None):
     """The dominant op under the four-stream load (largest device time per forward; `name`
     overrides the choice), and its roofline: algorithmic FLOPs (or bytes) per launch over its
@@ -246,6 +256,12 @@ def roofline(h, precision, model, reps=200, name=None):
               "traffic": t_bytes, "traffic_source": tsrc,
               "hbm_gbs": round(t_bytes / (ms * 1e-3) / 1e9, 1) if t_bytes else None,
               "mfma_busy_pct": mfma.get(name, {}).get("mfma_busy_pct"), "mfma_source": msrc}
+    rp = committed_rocprof(name)
+    if rp:  # the committed rocprofv3 --kernel-trace --stats average of the same launches
+        common["rocprof_avg_launch_ms"] = rp["avg_ms"]
+        common["frac_rocprof"] = round((flops / (rp["avg_ms"] * 1e-3) / 1e12 / peak) if flops else
+                                       (nbytes / (rp["avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS), 5)
+        common["rocprof_source"] = rp["source"]
     if loaded is not None:
         tot, cnt = loaded[name][0], loaded[name][1]
         fwd_loaded = sum(v[0] for v in loaded.values())

@@ -18,3 +18,4 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/
   python3 bench.py --roofline-only --roofline-op "$op" > "$out/roofline_only.json" 2> "$out/roofline_only.err"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof_bench" -- \
   python3 bench.py --extras 0 --cpu-seconds 0 > "$out/bench_prof.json" 2> "$out/bench_prof.err"
+python3 tools/rocprof_roofline.py "$(ls "$out"/prof/*/*_kernel_stats.csv | head -n 1)" "$op" "$out/roofline_rocprof.json"
