@@ -1164,13 +1164,13 @@ int estep_of(Prec prec) {
 // plan is evaluated three times per launch); spi_debug_gemm_reload_env()
 // re-reads them for in-process sweeps (tools/gemm_bench.py).
 //   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM
-//   SPI_GEMM_POLICY=latency | tput:T      plan rule (default tput:192)
+//   SPI_GEMM_POLICY=latency | tput:T      plan rule (default tput:128)
 //   SPI_GEMM_MAXSPLIT=S, SPI_GEMM_STAGES=N  caps for experiments
 struct Knobs {
   bool forced = false;
   Plan plan{};
   bool latency = false;
-  int target = 192;
+  int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
   int max_split = 0, stages = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
   int halo_stages = 3, halo_minh = 14;
@@ -1186,6 +1186,7 @@ struct Knobs {
   };
   HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
   int n_halo_map = 0;
+  int pair_joint = 1;   // SPI_GEMM_PAIR_JOINT=0: per-problem plans; 1: split-K of a grouped pair sized on both grids (launch_pair)
   int split_local = 0;  // SPI_GEMM_SPLIT_LOCAL=1: XCD-local split-K tiles reduce through L2
   int xcd2d = 2;  // 2-D tile -> XCD rectangles (xcd_groups); 2: not for split-K grids (plain order there)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
@@ -1214,6 +1215,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_PAIR_JOINT"); e && *e) k.pair_joint = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_BIG"); e && *e) k.big = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
@@ -1364,9 +1366,10 @@ int plan_tiles(const GemmDesc& d, const Plan& pl) {
 
 // Plan rule (default): the largest tile that still yields >= T workgroups,
 // split-K only when even 64x64 tiles fall short (then to ~T workgroups, >= 6
-// k-steps per slice).  T = 192 measured best with 4 concurrent worker streams
-// (ResNet-18 bs8 fp16x3 +8 %, ResNet-152 bs32 +8 %, BERT-base +5 %, ViT-L +7 %
-// over the latency rule; tools/gemm_bench.py / bench.py sweeps).
+// k-steps per slice).  T in 128..192 measured best with 4 concurrent worker
+// streams (ResNet-18 bs8 fp16x3 +8 %, ResNet-152 bs32 +8 %, BERT-base +5 %, ViT-L
+// +7 % over the latency rule; tools/gemm_bench.py / bench.py sweeps);
+// 128 since the joint pair plan (round 3).
 // SPI_GEMM_POLICY=latency keeps the single-stream rule: 64x64 tiles and
 // split-K to ~2 workgroups per CU.
 Plan choose_plan(const GemmDesc& d, Prec prec) {
@@ -1532,7 +1535,23 @@ void launch(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
 template <int MODE>
 void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, hipStream_t s) {
   const Prec pr = prec_of_mode(MODE);
-  const Plan q0 = choose_plan(d0, pr), q1 = choose_plan(d1, pr);
+  Plan q0 = choose_plan(d0, pr), q1 = choose_plan(d1, pr);
+  if (knobs().pair_joint && !q0.halo && !q1.halo && q0.splits > 1 && q0.bm == 64 && q0.bn == 64 &&
+      q1.bm == 64 && q1.bn == 64) {
+    // Joint plan: the grouped launch is one grid, so problem 1's workgroups count
+    // toward the T workgroups problem 0's split-K was sized for -- fewer slices,
+    // fewer fp32 slabs through memory.  Problem 1 (the 1x1 downsample, a few
+    // k-steps) takes problem 0's ring depth so the two still share a kernel.
+    const int ES = estep_of(pr), ksteps = d0.Kpad / ES;
+    const int t64 = plan_tiles(d0, q0), w1 = plan_tiles(d1, q1) * q1.splits;
+    const int T0 = std::max(1, knobs().target - w1);
+    const int sp = std::max(1, std::min({(T0 + t64 - 1) / t64, ksteps / 6, q0.splits}));
+    if (sp < q0.splits) {
+      const int kt = (ksteps + sp - 1) / sp;
+      q0 = finish_plan(Plan{64, 64, kt >= 16 ? 3 : 2, sp, 0}, ksteps, ES, d0.krep);
+      if (q1.splits == 1) q1.stages = q0.stages;
+    }
+  }
   KGroup g{};
   g.a[0] = make_args<MODE>(d0, p0, q0);
   GemmPtrs p1s = p1;
