@@ -31,8 +31,8 @@ def packed(prec, n, k):
     return torch.from_numpy(host).cuda()
 
 
-def plan_blocks(M, N, K, estep, T=192):
-    """Workgroups of the default plan rule (gemm.hip choose_plan, tput:T)."""
+def plan_blocks(M, N, K, estep, T=128):
+    """Workgroups of the default plan rule (gemm.hip choose_plan, tput:T, default 128)."""
     tiles = lambda bm, bn: -(-M // bm) * -(-N // bn)
     ks = -(-K // 64) * 64 // estep
     if N > 64 and tiles(128, 128) >= T:
