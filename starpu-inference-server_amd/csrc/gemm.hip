@@ -1177,6 +1177,8 @@ struct Knobs {
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
   int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
+  int st3_min = 16, st4_min = 1 << 20;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth)
+  int no_sq128 = 0;        // SPI_GEMM_NO128SQ=1: never 128x128 tiles (128x64 with a 3-stage ring instead)
   int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
@@ -1186,7 +1188,7 @@ struct Knobs {
   };
   HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
   int n_halo_map = 0;
-  int pair_joint = 1;   // SPI_GEMM_PAIR_JOINT=0: per-problem plans; 1: split-K of a grouped pair sized on both grids (launch_pair)
+  int pair_joint = 2;   // SPI_GEMM_PAIR_JOINT=0: per-problem plans; 1: split-K of a grouped pair sized on both grids; 2: + 128x64 pair tiles when the joint grid allows (launch_pair)
   int split_local = 0;  // SPI_GEMM_SPLIT_LOCAL=1: XCD-local split-K tiles reduce through L2
   int xcd2d = 2;  // 2-D tile -> XCD rectangles (xcd_groups); 2: not for split-K grids (plain order there)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
@@ -1217,6 +1219,9 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_PAIR_JOINT"); e && *e) k.pair_joint = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_BIG"); e && *e) k.big = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_ST3_MIN"); e && *e) k.st3_min = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_ST4_MIN"); e && *e) k.st4_min = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_NO128SQ"); e && *e) k.no_sq128 = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
@@ -1254,6 +1259,7 @@ Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
   if (pl.bm != 64 || pl.bn != 64) pl.splits = 1;  // split-K exists in the 64x64 kernels only
   if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
+  if (pl.bm == 128) pl.stages = pl.bn == 128 ? 2 : std::min(pl.stages, 3);  // the instantiated rings
   pl.splits = std::max(1, std::min(pl.splits, ksteps));
   int kt = (ksteps + pl.splits - 1) / pl.splits;
   kt = (kt + krep - 1) / krep * krep;  // krep: slices hold whole (hi, lo) step pairs
@@ -1378,7 +1384,9 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   const int ksteps = d.Kpad / ES;
   if (k.forced) return finish_plan(k.plan, ksteps, ES, d.krep);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
-  const auto stages_for = [](int kt) { return kt >= 16 ? 3 : 2; };  // a deeper ring pays only on long K loops
+  // a deeper ring pays only on long K loops (SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN: the k-steps from
+  // which 3 / 4 stages are used; 4 stages only reach the 64x64 tiles, finish_plan caps the others)
+  const auto stages_for = [&k](int kt) { return kt >= k.st4_min ? 4 : kt >= k.st3_min ? 3 : 2; };
   if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);  // one image per tile row
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
@@ -1391,7 +1399,7 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
       p.stages = 3;
       return p;
     }
-    if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
+    if (!k.no_sq128 && d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
     if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
     const int t64 = tiles_of(64, 64);
     const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
@@ -1550,6 +1558,18 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
       const int kt = (ksteps + sp - 1) / sp;
       q0 = finish_plan(Plan{64, 64, kt >= 16 ? 3 : 2, sp, 0}, ksteps, ES, d0.krep);
       if (q1.splits == 1) q1.stages = q0.stages;
+    }
+  }
+  if (knobs().pair_joint >= 2 && !q0.halo && !q1.halo && q0.splits == 1 && q1.splits == 1 && q0.bm == 64 &&
+      q0.bn == 64 && q1.bm == 64 && q1.bn == 64) {
+    // SPI_GEMM_PAIR_JOINT=2: the largest common tile whose joint grid still reaches T
+    // (the layer-2 pair: 98 + 98 tiles of 128 x 64 instead of 196 + 196 of 64 x 64)
+    const auto t = [](const GemmDesc& d, int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
+    if (t(d0, 128, 64) + t(d1, 128, 64) >= knobs().target) {
+      const int ES = estep_of(pr), k0 = d0.Kpad / ES, k1 = d1.Kpad / ES;
+      const int st = std::max(k0, k1) >= 16 ? 3 : 2;
+      q0 = finish_plan(Plan{128, 64, st, 1, 0}, k0, ES, d0.krep);
+      q1 = finish_plan(Plan{128, 64, st, 1, 0}, k1, ES, d1.krep);
     }
   }
   KGroup g{};
