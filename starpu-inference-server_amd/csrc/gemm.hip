@@ -232,11 +232,11 @@ __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
 // Separate instantiations keep each kind's loop free of the others.
 enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS = 4 };
 
-// Split-K is compiled into the 64x64 tiles and the halo kinds (no plan rule splits
-// another large tile; the reducer costs 36-120 VGPRs there).  Launch bounds ask
+// Split-K is compiled into the 64x64 and 128x64 tiles and the halo kinds (no plan
+// rule splits 128x128; the reducer costs 36-120 VGPRs there).  Launch bounds ask
 // for the occupancy each tile reaches within its registers: 4 / 3 / 2 waves per SIMD.
 template <int BM, int BN, int KIND>
-constexpr bool kSplitK = (BM == 64 && BN == 64) || KIND == kConvHalo || KIND == kConvHaloS;
+constexpr bool kSplitK = (BM == 64 && BN == 64) || (BM == 128 && BN == 64) || KIND == kConvHalo || KIND == kConvHaloS;
 
 // kConvHalo.  An implicit-GEMM conv stages each (tap, channel block) A tile
 // separately: every input pixel crosses the CU nine times, and the vector-memory
@@ -1177,7 +1177,9 @@ struct Knobs {
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
   int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
-  int st3_min = 16, st4_min = 1 << 20;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth)
+  int st3_min = 16, st4_min = 32;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth; 4 stages from 32
+                                   // k-steps: BERT-base FFN2 four-stream 20.8k -> 21.3k, ViT-L +-0)
+  int split128 = 0;        // SPI_GEMM_SPLIT128=1: 128x64 split-K plans (choose_plan)
   int no_sq128 = 0;        // SPI_GEMM_NO128SQ=1: never 128x128 tiles (128x64 with a 3-stage ring instead)
   int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
@@ -1222,6 +1224,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_ST3_MIN"); e && *e) k.st3_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_ST4_MIN"); e && *e) k.st4_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_NO128SQ"); e && *e) k.no_sq128 = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_SPLIT128"); e && *e) k.split128 = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
@@ -1257,7 +1260,7 @@ Knobs& knobs() {
 Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   const Knobs& k = knobs();
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
-  if (pl.bm != 64 || pl.bn != 64) pl.splits = 1;  // split-K exists in the 64x64 kernels only
+  if (pl.bn != 64 || (pl.bm != 64 && pl.bm != 128)) pl.splits = 1;  // split-K exists in the 64- and 128-row x 64 kernels only
   if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
   if (pl.bm == 128) pl.stages = pl.bn == 128 ? 2 : std::min(pl.stages, 3);  // the instantiated rings
   pl.splits = std::max(1, std::min(pl.splits, ksteps));
@@ -1401,6 +1404,13 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
     }
     if (!k.no_sq128 && d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
     if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
+    if (k.split128 && ksteps >= 16) {
+      // SPI_GEMM_SPLIT128=1: 128x64 tiles split over K to ~T workgroups (>= 8 k-steps per
+      // slice): a quarter fewer staged bytes per MFMA than 64x64 tiles, fp32 slabs twice as big
+      const int t128 = tiles_of(128, 64);
+      const int sp = std::min((T + t128 - 1) / t128, ksteps / 8);
+      if (sp >= 2) return finish_plan(Plan{128, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
+    }
     const int t64 = tiles_of(64, 64);
     const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
     return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
