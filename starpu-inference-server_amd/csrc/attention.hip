@@ -11,6 +11,8 @@
 // HF's BertModel adds).  head_dim is fixed at 64.
 #include "spi_kernels.hpp"
 
+#include <cstdlib>
+
 namespace spi {
 namespace {
 
@@ -201,13 +203,174 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv,
   }
 }
 
+// fp16, swapped orientation (round 3): S^T = K Q^T puts the key on the MFMA row and the
+// query on the lane (cdna_hip_programming.md §3, "An accumulator tile as the next MFMA's
+// operand"), so
+//   * a lane's softmax row is its own query: the row max / sum are the lane's 16 scores
+//     plus two xor shuffles (lanes 16 and 32 apart) instead of four per row;
+//   * P^T leaves the accumulators already shaped as the B operand of O^T = V^T P^T -- the
+//     fp32 -> fp16 conversion only, no LDS round trip for P (the round-2 kernel wrote P
+//     with 16 two-byte stores per lane per tile and read it back);
+//   * V stays row-major in LDS (16-byte stores, no scalar transpose on the way in) and
+//     V^T's A fragments come out of it by ds_read_b64_tr_b16 (T10): lane 4q + p of a
+//     16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block, lane i receives
+//     column i.  The k order inside a 32-key step is the accumulator's: element j of
+//     lane group g is key 16 (2 s + j / 4) + 4 g + j % 4, on both operands.
+// O^T's accumulator holds 4 consecutive head dims of one query per lane: 8-byte stores.
+__global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* __restrict__ qkv,
+                                                               const float* __restrict__ mask_bias,
+                                                               _Float16* __restrict__ ctx, int S, int H,
+                                                               float scale) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  typedef short short4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  constexpr int LD = HD + 8;  // K / V row stride in elements (144 B: 16-byte rows, 8-byte tr reads)
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[KT * LD];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[KT * LD];
+
+  const int D = H * HD, ld = 3 * D;
+  const int b = blockIdx.y / H, h = blockIdx.y % H;
+  const int q0 = blockIdx.x * QT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const _Float16* base = qkv + (size_t)b * S * ld;
+
+  // Q^T as the B operand: lane (fq, fr) holds Q[query fr][head dims 32 s + 8 fq ..]
+  const int qa = q0 + wave * 16 + fr;
+  half8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (qa < S) v = *reinterpret_cast<const half8*>(base + (size_t)qa * ld + h * HD + s * 32 + fq * 8);
+    qf[s] = v;
+  }
+  float m_q = -INFINITY, l_q = 0.f;  // this lane's query
+  floatx4 o[4];                      // o[dblk][r]: head dim 16 dblk + 4 fq + r of query fr
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int NCH = KT * HD / 8 / 256;  // 16-byte chunks of K (and of V) per thread per tile
+  uint4 kreg[NCH], vreg[NCH];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + i * 256;
+      const int key = c / (HD / 8), dc = c % (HD / 8);
+      const int kk = k0 + key;
+      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
+      if (kk < S) {
+        kreg[i] = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + D + h * HD + dc * 8);
+        vreg[i] = *reinterpret_cast<const uint4*>(base + (size_t)kk * ld + 2 * D + h * HD + dc * 8);
+      }
+    }
+  };
+  // tr-read addresses (byte offsets into Vs) of lane (fq, fr) for key half t of step s and
+  // head-dim block dblk: row 32 s + 16 t + 4 fq + fr / 4, columns 16 dblk + 4 (fr % 4)
+  const int tr_off = ((4 * fq + (fr >> 2)) * LD + 4 * (fr & 3)) * 2;
+  fetch(0);
+  for (int k0 = 0; k0 < S; k0 += KT) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous tile's reads are done
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + i * 256;
+      const int key = c / (HD / 8), dc = c % (HD / 8);
+      *reinterpret_cast<uint4*>(Ks + key * LD + dc * 8) = kreg[i];
+      *reinterpret_cast<uint4*>(Vs + key * LD + dc * 8) = vreg[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (k0 + KT < S) fetch(k0 + KT);
+
+    // S^T: sacc[j][r] = score of key k0 + 16 j + 4 fq + r for query fr
+    floatx4 sacc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sacc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const half8 kf = *reinterpret_cast<const half8*>(Ks + (j * 16 + fr) * LD + s * 32 + fq * 8);
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
+      }
+    }
+    float sc[4][4];
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + j * 16 + fq * 4 + r;
+        const float bias = key < S ? (mask_bias ? mask_bias[(size_t)b * S + key] : 0.f) : -INFINITY;
+        sc[j][r] = sacc[j][r] * scale + bias;
+        tmax = fmaxf(tmax, sc[j][r]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_q, tmax);
+    const float alpha = __expf(m_q - m_new);
+    float rs = 0.f;
+    half8 pf[2];  // P^T as the B operand of step s: element 4 t + r = key 16 (2 s + t) + 4 fq + r
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(sc[j][r] - m_new);
+        rs += p;
+        pf[j >> 1][(j & 1) * 4 + r] = static_cast<_Float16>(p);
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_q = l_q * alpha + rs;
+    m_q = m_new;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+
+    // O^T += V^T P^T
+    __attribute__((address_space(3))) char* vb = (__attribute__((address_space(3))) char*)Vs + tr_off;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const half4 lo = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(vb + ((32 * s) * LD + 16 * d) * 2)));
+        const half4 hi = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(vb + ((32 * s + 16) * LD + 16 * d) * 2)));
+        const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[s], o[d], 0, 0, 0);
+      }
+  }
+
+  if (qa < S) {
+    const float inv = 1.f / l_q;
+    _Float16* out = ctx + ((size_t)b * S + qa) * D + h * HD + fq * 4;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const half4 v = {static_cast<_Float16>(o[d][0] * inv), static_cast<_Float16>(o[d][1] * inv),
+                       static_cast<_Float16>(o[d][2] * inv), static_cast<_Float16>(o[d][3] * inv)};
+      *reinterpret_cast<half4*>(out + d * 16) = v;
+    }
+  }
+}
+
+int g_attn_swap = -1;  // SPI_ATTN_SWAP, read once (attention_reload_env re-reads it)
+int attn_variant() {
+  if (g_attn_swap < 0) {
+    const char* e = std::getenv("SPI_ATTN_SWAP");
+    g_attn_swap = e && *e ? std::atoi(e) : 1;
+  }
+  return g_attn_swap;
+}
+
 }  // namespace
+
+void attention_reload_env() { g_attn_swap = -1; }
 
 void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S, int heads,
                int hd, float scale, bool f16, hipStream_t s) {
   if (hd != HD) return;  // validated at model build time
   const dim3 grid((S + QT - 1) / QT, B * heads);
-  if (f16)
+  if (f16 && attn_variant())  // SPI_ATTN_SWAP=0: the round-2 orientation
+    hipLaunchKernelGGL(attn_f16_swapped_kernel, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
+                       (_Float16*)ctx, S, heads, scale);
+  else if (f16)
     hipLaunchKernelGGL((attn_kernel<_Float16>), grid, dim3(256), 0, s, (const _Float16*)qkv,
                        mask_bias, (_Float16*)ctx, S, heads, scale);
   else

@@ -283,6 +283,16 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
   float4 v[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] = xr[j * 64 + lane];
+  // gamma / beta issued with the row, not after the two reductions: one memory round trip
+  // fewer on the wave's dependent chain (the kernel is one such chain per row)
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4 gg[NV], bb[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    gg[j] = g4[j * 64 + lane];
+    bb[j] = b4[j * 64 + lane];
+  }
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < NV; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
@@ -294,17 +304,14 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
     q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  const float4* b4 = reinterpret_cast<const float4*>(b);
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c4 = j * 64 + lane;
-    const float4 gg = g4[c4], bb = b4[c4];
     float4 o;
-    o.x = (v[j].x - mean) * rstd * gg.x + bb.x;
-    o.y = (v[j].y - mean) * rstd * gg.y + bb.y;
-    o.z = (v[j].z - mean) * rstd * gg.z + bb.z;
-    o.w = (v[j].w - mean) * rstd * gg.w + bb.w;
+    o.x = (v[j].x - mean) * rstd * gg[j].x + bb[j].x;
+    o.y = (v[j].y - mean) * rstd * gg[j].y + bb[j].y;
+    o.z = (v[j].z - mean) * rstd * gg[j].z + bb[j].z;
+    o.w = (v[j].w - mean) * rstd * gg[j].w + bb[j].w;
     if (yf) reinterpret_cast<float4*>(yf + (size_t)row * ldy)[c4] = o;
     if (yt) {
       if constexpr (sizeof(T) == 2) {

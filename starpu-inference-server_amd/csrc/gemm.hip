@@ -1179,6 +1179,7 @@ struct Knobs {
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
   int st3_min = 16, st4_min = 32;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth; 4 stages from 32
                                    // k-steps: BERT-base FFN2 four-stream 20.8k -> 21.3k, ViT-L +-0)
+  int sq_stages = 2;       // SPI_GEMM_SQ_STAGES=3: 3-stage ring for dense fp16 128x128 tiles (96 KiB, one workgroup per CU)
   int split128 = 0;        // SPI_GEMM_SPLIT128=1: 128x64 split-K plans (choose_plan)
   int no_sq128 = 0;        // SPI_GEMM_NO128SQ=1: never 128x128 tiles (128x64 with a 3-stage ring instead)
   int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
@@ -1225,6 +1226,7 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_ST4_MIN"); e && *e) k.st4_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_NO128SQ"); e && *e) k.no_sq128 = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_SPLIT128"); e && *e) k.split128 = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_SQ_STAGES"); e && *e) k.sq_stages = std::atoi(e) == 3 ? 3 : 2;
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
@@ -1262,7 +1264,7 @@ Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
   if (pl.bn != 64 || (pl.bm != 64 && pl.bm != 128)) pl.splits = 1;  // split-K exists in the 64- and 128-row x 64 kernels only
   if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
-  if (pl.bm == 128) pl.stages = pl.bn == 128 ? 2 : std::min(pl.stages, 3);  // the instantiated rings
+  if (pl.bm == 128) pl.stages = pl.bn == 128 ? k.sq_stages : std::min(pl.stages, 3);  // the instantiated rings
   pl.splits = std::max(1, std::min(pl.splits, ksteps));
   int kt = (ksteps + pl.splits - 1) / pl.splits;
   kt = (kt + krep - 1) / krep * krep;  // krep: slices hold whole (hi, lo) step pairs
@@ -1507,6 +1509,8 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
   }
   if (pl.bm == 256)
     launch_tile<MODE, 256, 128, 3, 8>(g, grid, s);
+  else if (pl.bm == 128 && pl.bn == 128 && pl.stages == 3 && MODE == (int)Prec::F16 && !g.d.conv)
+    hipLaunchKernelGGL((gemm_kernel<MODE, 128, 128, 3, kDense>), grid, dim3(256), 0, s, g);  // SPI_GEMM_SQ_STAGES=3
   else if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(g, grid, s);
   else if (pl.bm == 128 && pl.stages == 2)
@@ -1622,6 +1626,7 @@ extern "C" void spi_debug_gemm_reload_env(void) {
   knobs() = read_knobs();
   conv_wres_reload_env();
   gemm256_reload_env();
+  attention_reload_env();
 }
 
 #ifdef SPI_GEMM_STAMPS

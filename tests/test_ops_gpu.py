@@ -83,7 +83,8 @@ def test_conv2d_nhwc(ops, prec, B, H, cin, cout, k, stride):
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("B,S,heads,masked", [(2, 128, 12, False), (3, 80, 4, True), (2, 197, 16, False),
-                                              (1, 5, 2, False), (2, 64, 2, True)])
+                                              (1, 5, 2, False), (2, 64, 2, True), (2, 197, 3, True),
+                                              (8, 128, 12, True)])
 def test_attention(ops, prec, B, S, heads, masked):
     g = torch.Generator().manual_seed(B * S + heads)
     D = heads * 64
@@ -103,15 +104,17 @@ def test_attention(ops, prec, B, S, heads, masked):
     assert err < tol, f"{prec} attention B{B} S{S} H{heads}: {err:.3e}"
 
 
-def test_attention_fully_masked_row(ops):
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_attention_fully_masked_row(ops, prec):
     """A fully masked row is uniform over the keys (finfo.min bias, as HF BERT)."""
     B, S, heads = 1, 16, 1
-    qkv = torch.randn(B * S, 3 * 64)
+    qkv = torch.randn(B * S, 3 * 64).to(ops.act_dtype(prec))
     bias = torch.full((B, S), torch.finfo(torch.float32).min)
-    ctx = ops.attention("fp32", qkv.cuda(), B, S, heads, mask_bias=bias.cuda())
-    v = qkv[:, 128:]
-    np.testing.assert_allclose(ctx.cpu().numpy(), v.mean(0, keepdim=True).expand(S, 64).numpy(), rtol=1e-5,
-                               atol=1e-5)
+    ctx = ops.attention(prec, qkv.cuda(), B, S, heads, mask_bias=bias.cuda())
+    v = qkv[:, 128:].float()
+    tol = 1e-5 if prec == "fp32" else 2e-3
+    np.testing.assert_allclose(ctx.float().cpu().numpy(), v.mean(0, keepdim=True).expand(S, 64).numpy(), rtol=tol,
+                               atol=tol)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
