@@ -217,7 +217,10 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv,
 //     column i.  The k order inside a 32-key step is the accumulator's: element j of
 //     lane group g is key 16 (2 s + j / 4) + 4 g + j % 4, on both operands.
 // O^T's accumulator holds 4 consecutive head dims of one query per lane: 8-byte stores.
-__global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* __restrict__ qkv,
+// NW waves per workgroup = 16 NW query rows: 4 (BERT) or 8 (ViT's S = 197: the K / V tiles are
+// staged once per 128 queries instead of per 64; 2 query tiles per head instead of 4).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float16* __restrict__ qkv,
                                                                const float* __restrict__ mask_bias,
                                                                _Float16* __restrict__ ctx, int S, int H,
                                                                float scale) {
@@ -230,7 +233,8 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
 
   const int D = H * HD, ld = 3 * D;
   const int b = blockIdx.y / H, h = blockIdx.y % H;
-  const int q0 = blockIdx.x * QT;
+  constexpr int NT = 64 * NW;
+  const int q0 = blockIdx.x * (16 * NW);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const _Float16* base = qkv + (size_t)b * S * ld;
@@ -249,12 +253,12 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
 #pragma unroll
   for (int d = 0; d < 4; ++d) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int NCH = KT * HD / 8 / 256;  // 16-byte chunks of K (and of V) per thread per tile
+  constexpr int NCH = KT * HD / 8 / NT;  // 16-byte chunks of K (and of V) per thread per tile
   uint4 kreg[NCH], vreg[NCH];
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * 256;
+      const int c = tid + i * NT;
       const int key = c / (HD / 8), dc = c % (HD / 8);
       const int kk = k0 + key;
       kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
@@ -267,12 +271,13 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
   // tr-read addresses (byte offsets into Vs) of lane (fq, fr) for key half t of step s and
   // head-dim block dblk: row 32 s + 16 t + 4 fq + fr / 4, columns 16 dblk + 4 (fr % 4)
   const int tr_off = ((4 * fq + (fr >> 2)) * LD + 4 * (fr & 3)) * 2;
+  const bool live = q0 + wave * 16 < S;  // wave-uniform
   fetch(0);
   for (int k0 = 0; k0 < S; k0 += KT) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous tile's reads are done
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * 256;
+      const int c = tid + i * NT;
       const int key = c / (HD / 8), dc = c % (HD / 8);
       *reinterpret_cast<uint4*>(Ks + key * LD + dc * 8) = kreg[i];
       *reinterpret_cast<uint4*>(Vs + key * LD + dc * 8) = vreg[i];
@@ -280,15 +285,23 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (k0 + KT < S) fetch(k0 + KT);
 
+    // A wave whose 16 queries all lie past S (ViT's last query tile: 5 of 64 rows) only
+    // stages; key blocks past S skip their MFMAs (their scores are -inf through the bias, so
+    // their P is 0 either way).  Both conditions are wave-uniform (EXEC stays full for the
+    // transposed reads).
+    if (!live) continue;
+    const int kleft = S - k0;
     // S^T: sacc[j][r] = score of key k0 + 16 j + 4 fq + r for query fr
     floatx4 sacc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       sacc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (j * 16 < kleft) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const half8 kf = *reinterpret_cast<const half8*>(Ks + (j * 16 + fr) * LD + s * 32 + fq * 8);
-        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
+        for (int s = 0; s < 2; ++s) {
+          const half8 kf = *reinterpret_cast<const half8*>(Ks + (j * 16 + fr) * LD + s * 32 + fq * 8);
+          sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
+        }
       }
     }
     float sc[4][4];
@@ -326,7 +339,8 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
     // O^T += V^T P^T
     __attribute__((address_space(3))) char* vb = (__attribute__((address_space(3))) char*)Vs + tr_off;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s) {
+      if (s * 32 >= kleft) break;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const half4 lo = __builtin_bit_cast(
@@ -336,6 +350,7 @@ __global__ __launch_bounds__(256) void attn_f16_swapped_kernel(const _Float16* _
         const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         o[d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[s], o[d], 0, 0, 0);
       }
+    }
   }
 
   if (qa < S) {
@@ -367,9 +382,15 @@ void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S,
                int hd, float scale, bool f16, hipStream_t s) {
   if (hd != HD) return;  // validated at model build time
   const dim3 grid((S + QT - 1) / QT, B * heads);
-  if (f16 && attn_variant())  // SPI_ATTN_SWAP=0: the round-2 orientation
-    hipLaunchKernelGGL(attn_f16_swapped_kernel, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
+  const int av = attn_variant();
+  if (f16 && av && (av == 2 || (av == 1 && S > 128))) {  // SPI_ATTN_SWAP=0: the round-2 orientation
+    const dim3 g8((S + 127) / 128, B * heads);
+    hipLaunchKernelGGL(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
+  } else if (f16 && av) {
+    hipLaunchKernelGGL(attn_f16_swapped_kernel<4>, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
+                       (_Float16*)ctx, S, heads, scale);
+  }
   else if (f16)
     hipLaunchKernelGGL((attn_kernel<_Float16>), grid, dim3(256), 0, s, (const _Float16*)qkv,
                        mask_bias, (_Float16*)ctx, S, heads, scale);

@@ -1177,6 +1177,11 @@ struct Knobs {
   int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
   int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
+  // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
+  // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
+  // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
+  // GEMMs stay off: -1.3 % with them)
+  int g256_longk_tiles = 48, g256_longk_k = 1024;
   int st3_min = 16, st4_min = 32;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth; 4 stages from 32
                                    // k-steps: BERT-base FFN2 four-stream 20.8k -> 21.3k, ViT-L +-0)
   int sq_stages = 2;       // SPI_GEMM_SQ_STAGES=3: 3-stage ring for dense fp16 128x128 tiles (96 KiB, one workgroup per CU)
@@ -1228,6 +1233,15 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_SPLIT128"); e && *e) k.split128 = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_SQ_STAGES"); e && *e) k.sq_stages = std::atoi(e) == 3 ? 3 : 2;
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_256_LONGK"); e && *e) {
+    int t = 0, kk = 0;
+    if (std::sscanf(e, "%d,%d", &t, &kk) == 2) {
+      k.g256_longk_tiles = t;
+      k.g256_longk_k = kk;
+    } else {
+      k.g256_longk_tiles = 0;  // e.g. "0": off
+    }
+  }
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
     // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
     // (OW 0 = any other width; rows 0 = not a halo conv)
@@ -1678,7 +1692,10 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
     case Prec::F16:
       if (conv_wres_eligible(d, prec, p))
         conv_wres(d, p, s);
-      else if (gemm256_eligible(d, prec, knobs().g256_min) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
+      else if ((gemm256_eligible(d, prec, knobs().g256_min) ||
+                (knobs().g256_longk_tiles > 0 && d.K >= knobs().g256_longk_k &&
+                 gemm256_eligible(d, prec, knobs().g256_longk_tiles))) &&
+               (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
           (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
         gemm256(d, p, s);
       else
