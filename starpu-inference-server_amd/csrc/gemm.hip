@@ -679,12 +679,25 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[it][e] = apply_act(y[it][e], act);
       };
-      if (d.act == Act::Relu)
+      if (d.act == Act::Relu) {
         apply(std::integral_constant<Act, Act::Relu>{});
-      else if (d.act == Act::Gelu)
+      } else if (d.act == Act::Gelu && fmt == 0) {
+        // fp16 output: the packed degree-7/6 GELU (device_math.hpp gelu2, |erf error| 2.5e-6, 80x
+        // under an fp16 half-ulp) at half the VALU of the scalar 13/8 form; fp32 / split outputs
+        // keep the 4.5e-7 form (fp32 parity bar)
+#pragma unroll
+        for (int it = 0; it < NI; ++it)
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const float2v g2 = gelu2(float2v{y[it][e], y[it][e + 1]});
+            y[it][e] = g2.x;
+            y[it][e + 1] = g2.y;
+          }
+      } else if (d.act == Act::Gelu) {
         apply(std::integral_constant<Act, Act::Gelu>{});
-      else
+      } else {
         apply(std::integral_constant<Act, Act::None>{});
+      }
     };
     float b[8];
     if (a.vec_ok && n0 + BN <= d.N) {
