@@ -359,9 +359,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     for (int e = 0; e < 8; ++e) bias8[e] = 0.f;
   }
   // activation and output format are dispatched once, outside the rounds
-  auto epi = [&](auto act_c, auto f32_c) {
+  auto epi = [&](auto act_c, auto f32_c, auto guard_c) {
     constexpr int ACT = decltype(act_c)::value;
     constexpr bool OUTF32 = decltype(f32_c)::value;
+    constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // residual rows: the first half of the round's prefetched, the rest loaded inside the
@@ -446,10 +447,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
               y[e + 1] = g2.y;
             }
           }
-          // rows past M store to row M - 1: their A rows were loaded clamped to M - 1 (and their
-          // residual rows too), so the values are bit-identical to that row's -- a duplicate
-          // write instead of a branch around each pass's stores
-          const size_t ci = (size_t)min(m, g.M - 1) * g.ldc + nb;
+          // Rows past M exist only in tiles that cross M (GUARD, the last tile row): their stores
+          // are skipped.  (Storing them as duplicates of row M - 1, as full tiles' branch-free walk
+          // could, races with the real row M - 1 when C is the residual buffer itself -- the
+          // transformer's in-place residual stream: a duplicate that reads the residual after the
+          // real row's store adds the GEMM twice.)
+          if constexpr (GUARD) {
+            if (m >= g.M) continue;
+          }
+          const size_t ci = (size_t)m * g.ldc + nb;
           if constexpr (OUTF32) {
             *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci) = floatx4{y[0], y[1], y[2], y[3]};
             *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci + 4) = floatx4{y[4], y[5], y[6], y[7]};
@@ -463,13 +469,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 };
+  auto by_guard = [&](auto act_c, auto f32_c) {
+    if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
+      epi(act_c, f32_c, std::false_type{});
+    else
+      epi(act_c, f32_c, std::true_type{});
+  };
   auto by_act = [&](auto f32_c) {
     if (act == Act::Gelu)
-      epi(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
     else if (act == Act::Relu)
-      epi(std::integral_constant<int, (int)Act::Relu>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::Relu>{}, f32_c);
     else
-      epi(std::integral_constant<int, (int)Act::None>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c);
   };
   if (g.out_f32)
     by_act(std::true_type{});

@@ -364,6 +364,32 @@ def test_gemm256_tiles(ops, gemm256_everywhere, M, N, K, act, res, out_f32):
     assert err < (1e-5 if out_f32 else 2e-3), f"gemm256 {M}x{N}x{K} {act} {res}: {err:.3e}"
 
 
+@pytest.mark.parametrize("router", ["everywhere", "longk"])
+@pytest.mark.parametrize("M,N,K", [(3152, 1024, 4096), (3152, 1024, 1024), (300, 512, 128)])
+def test_gemm256_in_place_residual(ops, gemm256_everywhere, router, M, N, K):
+    """C is the fp32 residual buffer itself (the transformer's residual stream, updated in place)
+    and M is ragged: rows past M in the last tile row must not be stored (a duplicate store of row
+    M - 1 races with the real one and can add the GEMM twice).  `longk` runs with the default
+    routing (SPI_GEMM_256_LONGK: ViT-L's FFN2 / out-projection shapes)."""
+    import os
+    if router == "longk":
+        os.environ.pop("SPI_GEMM_256_MIN", None)
+        ops.lib.spi_debug_gemm_reload_env()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).half()
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    ref = A.float() @ W.half().float().T + b + R
+    Rd = R.cuda()
+    for _ in range(3):  # the race shows up on some launches only
+        Rd.copy_(R.cuda())
+        ops.gemm("fp16", A.cuda(), ops.pack_weight("fp16", W), N, bias=b.cuda(), residual=Rd, out=Rd, out_f32=True)
+        torch.cuda.synchronize()
+        err = normalized_max_error(Rd.cpu().numpy(), ref.numpy())
+        assert err < 1e-5, f"in-place gemm {M}x{N}x{K} ({router}): {err:.3e}"
+
+
 def test_gemm256_unaligned_output(ops, gemm256_everywhere):
     """An output buffer off 16-byte alignment takes gemm256's per-element epilogue."""
     M, N, K = 300, 512, 128
