@@ -1198,6 +1198,7 @@ struct Knobs {
   int st3_min = 16, st4_min = 32;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth; 4 stages from 32
                                    // k-steps: BERT-base FFN2 four-stream 20.8k -> 21.3k, ViT-L +-0)
   int sq_stages = 2;       // SPI_GEMM_SQ_STAGES=3: 3-stage ring for dense fp16 128x128 tiles (96 KiB, one workgroup per CU)
+  int dlk_k = 0, dlk_t = 0;  // SPI_GEMM_DENSE_LONGK_T="K,T" (choose_plan)
   int split128 = 0;        // SPI_GEMM_SPLIT128=1: 128x64 split-K plans (choose_plan)
   int no_sq128 = 0;        // SPI_GEMM_NO128SQ=1: never 128x128 tiles (128x64 with a 3-stage ring instead)
   int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
@@ -1244,6 +1245,9 @@ Knobs read_knobs() {
   if (const char* e = std::getenv("SPI_GEMM_ST4_MIN"); e && *e) k.st4_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_NO128SQ"); e && *e) k.no_sq128 = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_SPLIT128"); e && *e) k.split128 = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_DENSE_LONGK_T"); e && *e) {
+    if (std::sscanf(e, "%d,%d", &k.dlk_k, &k.dlk_t) != 2 || k.dlk_t < 1) k.dlk_k = 0;
+  }
   if (const char* e = std::getenv("SPI_GEMM_SQ_STAGES"); e && *e) k.sq_stages = std::atoi(e) == 3 ? 3 : 2;
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_LONGK"); e && *e) {
@@ -1422,7 +1426,9 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);  // one image per tile row
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   if (!k.latency) {
-    const int T = k.target;
+    // SPI_GEMM_DENSE_LONGK_T="K,T": dense GEMMs with Kpad >= K plan for T workgroups (fewer,
+    // larger tiles on long K loops)
+    const int T = (!d.conv && k.dlk_k > 0 && d.Kpad >= k.dlk_k) ? k.dlk_t : k.target;
     // 256x128 tiles, 8 waves (2 per SIMD), 3 stages: a quarter fewer staging
     // instructions per MFMA than 128x128 (SPI_GEMM_BIG=1; off by default: ViT-L -4 %, 4096^3 -3 %)
     if (k.big && d.N > 64 && !d.pool_rows && tiles_of(256, 128) >= T) {
