@@ -118,7 +118,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 // LDS map: halo buffers at 0 and kHBuf (A fragment reads then use an immediate
 // offset per buffer), the resident weights from 2 * kHBuf.
 
-template <bool HAS_RES, bool RELU, int NBUF>
+// WLA (one-band workgroups): weight taps in flight ahead of the tap being computed -- 9: all 72
+// pieces go out behind the halo at the start; fewer: taps 0..WLA-1 up front, tap T + WLA - 1 issued
+// when tap T starts, so the first tap's wait covers the halo and WLA taps instead of all nine.
+template <bool HAS_RES, bool RELU, int NBUF, int WLA = 9>
 __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   constexpr int kW0 = NBUF * kHBuf;
   __shared__ __attribute__((aligned(16))) char lds[kLds<NBUF>];
@@ -155,6 +158,13 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     }
   };
   if constexpr (NBUF == 2) issue_w();
+  auto issue_wtap = [&](int tap) {  // NBUF 1 order: tap t is pieces 8 t .. 8 t + 7, two per wave
+#pragma unroll
+    for (int i = 2 * tap; i < 2 * tap + 2; ++i) {
+      const int q = i * 4 + wave;
+      glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
+    }
+  };
 
   // ---- halo bookkeeping, band-independent: piece i of this wave fills pixels
   // p = (wave * 8 + i) * 8 + lane / 8, slot lane % 8 <- chunk slot ^ (p & 7)
@@ -236,7 +246,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     // buffer: only after this band's epilogue
     if (NBUF == 2 && next) issue_halo(band + 1, BUF ^ 1);
     if (NBUF == 1)
-      dma_wait_barrier<2 * 8>();  // the halo and tap 0 have landed (taps 1..8 still in flight)
+      dma_wait_barrier<2 * (WLA >= 9 ? 8 : WLA - 1)>();  // the halo and tap 0 have landed
     else if (next)
       dma_wait_barrier<kHPieces>();  // everything but the next halo has landed
     else
@@ -263,7 +273,15 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
       constexpr int t = decltype(tc)::value;
       if constexpr (t + 1 < 18) {
         // one-band workgroups: tap (t + 1) / 2's weight pieces land while taps before it compute
-        if constexpr (NBUF == 1 && (t + 1) % 2 == 0) dma_wait_barrier<2 * (8 - (t + 1) / 2)>();
+        if constexpr (NBUF == 1 && (t + 1) % 2 == 0) {
+          constexpr int T = (t + 1) / 2;  // the tap that starts here
+          if constexpr (WLA >= 9) {
+            dma_wait_barrier<2 * (8 - T)>();
+          } else {
+            if constexpr (T + WLA - 1 <= 8) issue_wtap(T + WLA - 1);
+            dma_wait_barrier<2 * ((WLA - 1) < (8 - T) ? (WLA - 1) : (8 - T))>();
+          }
+        }
         load(t + 1, (t + 1) & 1);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -346,7 +364,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
 
   issue_halo(b_first, 0);
   if constexpr (NBUF == 1) {  // one band per workgroup
-    issue_w();
+    if constexpr (WLA >= 9) {
+      issue_w();
+    } else {
+#pragma unroll
+      for (int tap = 0; tap < WLA; ++tap) issue_wtap(tap);
+    }
     band_body(std::integral_constant<int, 0>{}, b_first, false, 1);
   } else {
     for (int j = 0; j < nb; j += 2) {
@@ -369,10 +392,11 @@ int env_int(const char* name, int dflt) {
 // SPI_CONV_WRES_NBUF=2: the double-buffered kernel even for one band per workgroup.
 // Read once; conv_wres_reload_env() (spi_debug_gemm_reload_env) re-reads them for sweeps.
 struct WresKnobs {
-  int on = 1, bpw = 0, nbuf = 0;
+  int on = 1, bpw = 0, nbuf = 0, wla = 9;
 };
 WresKnobs read_wres_knobs() {
-  return WresKnobs{env_int("SPI_CONV_WRES", 1), env_int("SPI_CONV_WRES_BPW", 0), env_int("SPI_CONV_WRES_NBUF", 0)};
+  return WresKnobs{env_int("SPI_CONV_WRES", 1), env_int("SPI_CONV_WRES_BPW", 0), env_int("SPI_CONV_WRES_NBUF", 0),
+                   env_int("SPI_CONV_WRES_WLA", 9)};
 }
 WresKnobs& wres_knobs() {
   static WresKnobs k = read_wres_knobs();
@@ -432,14 +456,16 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   // double-buffered kernel (SPI_CONV_WRES_NBUF=2 forces it for one band too)
   const bool two = a.bpw > 1 || wres_knobs().nbuf == 2;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, s, a); };
+  // SPI_CONV_WRES_WLA=3: weight taps streamed 3 ahead of the computing tap (one-band kind only)
+  const bool la = !two && wres_knobs().wla < 9;
   if (a.res && relu)
-    two ? go(conv3x3_c64_wres<true, true, 2>) : go(conv3x3_c64_wres<true, true, 1>);
+    two ? go(conv3x3_c64_wres<true, true, 2>) : la ? go(conv3x3_c64_wres<true, true, 1, 3>) : go(conv3x3_c64_wres<true, true, 1>);
   else if (a.res)
-    two ? go(conv3x3_c64_wres<true, false, 2>) : go(conv3x3_c64_wres<true, false, 1>);
+    two ? go(conv3x3_c64_wres<true, false, 2>) : la ? go(conv3x3_c64_wres<true, false, 1, 3>) : go(conv3x3_c64_wres<true, false, 1>);
   else if (relu)
-    two ? go(conv3x3_c64_wres<false, true, 2>) : go(conv3x3_c64_wres<false, true, 1>);
+    two ? go(conv3x3_c64_wres<false, true, 2>) : la ? go(conv3x3_c64_wres<false, true, 1, 3>) : go(conv3x3_c64_wres<false, true, 1>);
   else
-    two ? go(conv3x3_c64_wres<false, false, 2>) : go(conv3x3_c64_wres<false, false, 1>);
+    two ? go(conv3x3_c64_wres<false, false, 2>) : la ? go(conv3x3_c64_wres<false, false, 1, 3>) : go(conv3x3_c64_wres<false, false, 1>);
 }
 
 }  // namespace spi
