@@ -240,12 +240,14 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   // address plus an immediate).  The k-loop keeps chunk t + 1's six fragment reads in
   // flight behind chunk t's eight MFMAs (sched_barrier pins the order; the compiler's
   // counted lgkmcnt then waits only for chunk t).
-  auto band_body = [&](auto buf_c, int band, bool next, int sk) {
+  auto band_body = [&](auto buf_c, int band, bool next, int sk, bool first = true) {
     constexpr int BUF = decltype(buf_c)::value;
     // the next band's halo into the buffer band - 1 used (its epilogue ended in a barrier); one
     // buffer: only after this band's epilogue
     if (NBUF == 2 && next) issue_halo(band + 1, BUF ^ 1);
-    if (NBUF == 1)
+    if (NBUF == 1 && !first)
+      dma_wait_barrier<0>();  // a later band of a one-buffer workgroup: its halo (weights are resident)
+    else if (NBUF == 1)
       dma_wait_barrier<2 * (WLA >= 9 ? 8 : WLA - 1)>();  // the halo and tap 0 have landed
     else if (next)
       dma_wait_barrier<kHPieces>();  // everything but the next halo has landed
@@ -371,6 +373,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
       for (int tap = 0; tap < WLA; ++tap) issue_wtap(tap);
     }
     band_body(std::integral_constant<int, 0>{}, b_first, false, 1);
+    // several bands on one buffer (SPI_CONV_WRES_NBUF=1 with SPI_CONV_WRES_BPW > 1): the weights stay,
+    // each later band's halo goes into the buffer the previous epilogue released (exposed load)
+    for (int j = 1; j < nb; ++j) {
+      issue_halo(b_first + j, 0);
+      band_body(std::integral_constant<int, 0>{}, b_first + j, false, -1, false);
+    }
   } else {
     for (int j = 0; j < nb; j += 2) {
       band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
@@ -454,7 +462,7 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   const int grid = (a.bands + a.bpw - 1) / a.bpw;
   // one band per workgroup: one halo buffer (104 KiB of LDS); several bands: the
   // double-buffered kernel (SPI_CONV_WRES_NBUF=2 forces it for one band too)
-  const bool two = a.bpw > 1 || wres_knobs().nbuf == 2;
+  const bool two = wres_knobs().nbuf == 2 || (a.bpw > 1 && wres_knobs().nbuf != 1);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, s, a); };
   // SPI_CONV_WRES_WLA=3: weight taps streamed 3 ahead of the computing tap (one-band kind only)
   const bool la = !two && wres_knobs().wla < 9;
