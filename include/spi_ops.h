@@ -27,7 +27,12 @@ extern "C" {
 
 /* Packed weight layout for a [N][K] fp32 matrix: rows padded to Npad = 128k,
  * columns to Kpad = 64k; fp16 / fp32 elements, or for fp16x3 (2 and 3) per
- * 32-k block [32 hi fp16 | 32 lo fp16].  Returns the packed byte count; writes Npad/Kpad. */
+ * 32-k block [32 hi fp16 | 32 lo fp16].  Returns the packed byte count; writes Npad/Kpad.
+ * One exception to "zero padded": an fp16 [64][576] matrix (a 3x3 conv over 64 channels)
+ * carries, in its padding rows 64..127, the weight-resident conv's LDS image of rows 0..63
+ * (per tap t, row n, 16-byte slot s: chunk s ^ (n & 7) of row n's taps-t block), and
+ * spi_op_conv2d routes such convs to that kernel, which reads those rows.  Packed weights
+ * for spi_op_conv2d / spi_op_gemm must therefore come from spi_op_pack_weight, whole. */
 size_t spi_op_packed_bytes(int32_t precision, int32_t N, int32_t K, int32_t* Npad, int32_t* Kpad);
 /* Host-side packing: w_host fp32 [N][K] -> dst_host (spi_op_packed_bytes bytes). */
 int spi_op_pack_weight(int32_t precision, const float* w_host, int32_t N, int32_t K, void* dst_host);

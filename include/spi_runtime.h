@@ -166,7 +166,10 @@ typedef struct spi_runtime_config {
   int32_t warmup_batches;     /* per-worker warm-up at create (inference_runner.cpp:507-560):
                                  0 = every batch size 1..max_batch captured before serving (no
                                  capture on a live request), k > 0 = batch sizes 1..k and max_batch,
-                                 -1 = max_batch only */
+                                 -1 = max_batch only.  Cost: one hipGraph capture per (worker,
+                                 batch size), serialised process-wide -- e.g. 4 workers x 32 sizes
+                                 per device for ResNet-152 bs32; a zeroed struct asks for all of
+                                 them.  spi_runtime_warmup_seconds() reports what it took. */
   int32_t _pad0;
 } spi_runtime_config;
 
@@ -206,6 +209,8 @@ int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out
 int32_t spi_runtime_h2d_mode(const spi_runtime* rt);
 /* Current adaptive target batch limit (samples); the fixed limit otherwise. */
 int32_t spi_runtime_batch_target(const spi_runtime* rt);
+/* Wall time spi_runtime_create spent in the per-worker warm-up (graph captures, workspaces). */
+double spi_runtime_warmup_seconds(const spi_runtime* rt);
 void spi_runtime_destroy(spi_runtime* rt);
 
 /* ---------------------------------------------------------------------------

@@ -365,38 +365,28 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
   }
 }
 
-int g_attn_swap = -1;  // SPI_ATTN_SWAP, read once (attention_reload_env re-reads it)
-int attn_variant() {
-  if (g_attn_swap < 0) {
-    const char* e = std::getenv("SPI_ATTN_SWAP");
-    g_attn_swap = e && *e ? std::atoi(e) : 1;
-  }
-  return g_attn_swap;
-}
-
 }  // namespace
 
-void attention_reload_env() { g_attn_swap = -1; }
+void attention_reload_env() {}
 
+// fp16: the swapped orientation, 8-wave workgroups of 128 queries for S > 128 (ViT-L's 197),
+// 4 waves of 64 queries otherwise; fp32: the round-2 orientation (the round-2 fp16 kernel
+// and the forced 4 / 8-wave variants were removed in round 4).
 void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S, int heads,
                int hd, float scale, bool f16, hipStream_t s) {
   if (hd != HD) return;  // validated at model build time
   const dim3 grid((S + QT - 1) / QT, B * heads);
-  const int av = attn_variant();
-  if (f16 && av && (av == 2 || (av == 1 && S > 128))) {  // SPI_ATTN_SWAP=0: the round-2 orientation
+  if (f16 && S > 128) {
     const dim3 g8((S + 127) / 128, B * heads);
     hipLaunchKernelGGL(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
-  } else if (f16 && av) {
+  } else if (f16) {
     hipLaunchKernelGGL(attn_f16_swapped_kernel<4>, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
-  }
-  else if (f16)
-    hipLaunchKernelGGL((attn_kernel<_Float16>), grid, dim3(256), 0, s, (const _Float16*)qkv,
-                       mask_bias, (_Float16*)ctx, S, heads, scale);
-  else
+  } else {
     hipLaunchKernelGGL((attn_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv,
                        mask_bias, (float*)ctx, S, heads, scale);
+  }
 }
 
 }  // namespace spi

@@ -11,10 +11,9 @@
 // halo buffers.  Here a workgroup
 //   * DMAs the 72 KiB of weights ONCE (per-tap images in the ring's swizzled
 //     [row][128 B] layout, chunk c of row n at slot c ^ (n & 7)),
-//   * walks `bpw` bands of `th` whole output rows (the kConvHalo band: th rows x
-//     W pixels as tile rows 0..127), DMAing each band's (th + 2) x (W + 2) input
-//     pixels once into one of two halo buffers -- band j + 1's halo is issued
-//     before band j computes, so it lands behind 144 MFMAs per wave,
+//   * owns one band of `th` whole output rows (the kConvHalo band: th rows x
+//     W pixels as tile rows 0..127), DMAing its (th + 2) x (W + 2) input pixels
+//     once into the halo buffer, ahead of the weights, tap by tap,
 //   * computes all 9 taps x 64 channels from LDS with no global access in the
 //     k-loop (A fragments at halo pixel offset kh * (W + 2) + kw, B fragments
 //     from the resident tap image),
@@ -43,11 +42,11 @@ constexpr int kWImg = 64 * kRowB;           // one tap's [64 cout][64 cin] image
 constexpr int kWBytes = 9 * kWImg;          // 72 KiB resident weights
 constexpr int kHaloPix = 256;               // halo buffer capacity in pixels
 constexpr int kHBuf = kHaloPix * kRowB;     // 32 KiB (also the 128 x 64 fp32 epilogue tile)
-// LDS: NBUF halo buffers (2: the next band's halo streams in during this band's k-loop;
-// 1: one band per workgroup) + the resident weights -- 136 / 104 KiB.  With one buffer a
-// 48 KiB workgroup of another worker stream's kernel still fits beside it on the CU.
-template <int NBUF>
-constexpr int kLds = NBUF * kHBuf + kWBytes;
+// LDS: the halo buffer + the resident weights -- 104 KiB, so a 48 KiB workgroup of
+// another worker stream's kernel still fits beside it on the CU.  (Several bands per
+// workgroup -- one halo buffer reused, or two double-buffered -- measured -1 % / -5 % at
+// four streams and were removed in round 4)
+constexpr int kLds = kHBuf + kWBytes;
 constexpr int BM = 128, BN = 64, NT = 256;  // tile rows (pixels of a band), columns, threads
 constexpr int kWPieces = kWBytes / 1024 / 4;   // 18 weight DMA pieces per wave
 constexpr int kHPieces = kHBuf / 1024 / 4;     // 8 halo DMA pieces per wave
@@ -61,7 +60,7 @@ struct WresArgs {
   const char* zeros;    // >= 256 zero bytes
   int H, W;             // input = output size
   int th;               // output rows per band
-  int bands_per_img, bands, bpw;
+  int bands_per_img, bands;
 };
 
 __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
@@ -115,16 +114,11 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// LDS map: halo buffers at 0 and kHBuf (A fragment reads then use an immediate
-// offset per buffer), the resident weights from 2 * kHBuf.
-
-// WLA (one-band workgroups): weight taps in flight ahead of the tap being computed -- 9: all 72
-// pieces go out behind the halo at the start; fewer: taps 0..WLA-1 up front, tap T + WLA - 1 issued
-// when tap T starts, so the first tap's wait covers the halo and WLA taps instead of all nine.
-template <bool HAS_RES, bool RELU, int NBUF, int WLA = 9>
+// LDS map: the halo buffer at 0, the resident weights from kHBuf.
+template <bool HAS_RES, bool RELU>
 __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
-  constexpr int kW0 = NBUF * kHBuf;
-  __shared__ __attribute__((aligned(16))) char lds[kLds<NBUF>];
+  constexpr int kW0 = kHBuf;
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware band order: the hardware deals consecutive workgroups round-robin to the 8
   // XCDs; remapped, each XCD walks a contiguous run of bands, so the two input rows that
@@ -135,9 +129,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = wg & 7, l = wg >> 3;
     if (nwg >= 16) wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
   }
-  const int b_first = wg * a.bpw;
-  const int nb = min(a.bpw, a.bands - b_first);
-  if (nb <= 0) return;  // uniform per workgroup
+  const int band = wg;
+  if (band >= a.bands) return;  // uniform per workgroup
   const int Wp = a.W + 2;
   const int hp = (a.th + 2) * Wp;
 #ifdef SPI_WRES_STAMPS
@@ -146,22 +139,14 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
   WRES_STAMP(0);
 
   // ---- resident weights: the packed matrix's padding rows hold the LDS image (pack.hpp:
-  // pack_matrix_into), 72 contiguous pieces of 1 KiB, 18 per wave.  One-band workgroups
-  // (NBUF 1) issue them after the band's halo, two pieces per tap per wave in tap order, and
-  // start each tap as soon as its pieces have landed; the others issue them first.
+  // pack_matrix_into), 72 contiguous pieces of 1 KiB, 18 per wave, issued after the band's
+  // halo, two pieces per tap per wave in tap order: each tap starts as soon as its pieces
+  // have landed.
   const char* wimg = a.w + (size_t)64 * (9 * kRowB);
   auto issue_w = [&] {
 #pragma unroll
     for (int i = 0; i < kWPieces; ++i) {
-      const int q = NBUF == 1 ? i * 4 + wave : wave * kWPieces + i;
-      glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
-    }
-  };
-  if constexpr (NBUF == 2) issue_w();
-  auto issue_wtap = [&](int tap) {  // NBUF 1 order: tap t is pieces 8 t .. 8 t + 7, two per wave
-#pragma unroll
-    for (int i = 2 * tap; i < 2 * tap + 2; ++i) {
-      const int q = i * 4 + wave;
+      const int q = i * 4 + wave;  // tap t is pieces 8 t .. 8 t + 7
       glds16(wimg + q * 1024 + lane * 16, lds + kW0 + q * 1024);
     }
   };
@@ -179,10 +164,10 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     h_ok[i] = p < hp && (unsigned)(hx - 1) < (unsigned)a.W;
     h_off[i] = ((hy - 1) * a.W + (hx - 1)) * 64 + c * 8;  // elements from the band's (oy0, 0) pixel
   }
-  auto issue_halo = [&](int band, int buf) {
+  auto issue_halo = [&] {
     const int img = band / a.bands_per_img, oy0 = (band - img * a.bands_per_img) * a.th;
     const _Float16* base = a.x + ((size_t)img * a.H + oy0) * a.W * 64;
-    char* dst = lds + buf * kHBuf;
+    char* dst = lds;
 #pragma unroll
     for (int i = 0; i < kHPieces; ++i) {
       const int iy = oy0 - 1 + h_hy[i];
@@ -236,25 +221,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     e_rel[it] = ty * a.W + tx;
   }
 
-  // One band on halo buffer BUF (a compile-time constant: every fragment read is a VGPR
-  // address plus an immediate).  The k-loop keeps chunk t + 1's six fragment reads in
-  // flight behind chunk t's eight MFMAs (sched_barrier pins the order; the compiler's
-  // counted lgkmcnt then waits only for chunk t).
-  auto band_body = [&](auto buf_c, int band, bool next, int sk, bool first = true) {
-    constexpr int BUF = decltype(buf_c)::value;
-    // the next band's halo into the buffer band - 1 used (its epilogue ended in a barrier); one
-    // buffer: only after this band's epilogue
-    if (NBUF == 2 && next) issue_halo(band + 1, BUF ^ 1);
-    if (NBUF == 1 && !first)
-      dma_wait_barrier<0>();  // a later band of a one-buffer workgroup: its halo (weights are resident)
-    else if (NBUF == 1)
-      dma_wait_barrier<2 * (WLA >= 9 ? 8 : WLA - 1)>();  // the halo and tap 0 have landed
-    else if (next)
-      dma_wait_barrier<kHPieces>();  // everything but the next halo has landed
-    else
-      dma_wait_barrier<0>();
-    if (sk >= 0) WRES_STAMP(sk);
-    const char* Hs = lds + BUF * kHBuf;
+  // The band (every fragment read is a VGPR address plus an immediate).  The k-loop keeps
+  // chunk t + 1's six fragment reads in flight behind chunk t's eight MFMAs (sched_barrier
+  // pins the order; the compiler's counted lgkmcnt then waits only for chunk t).
+  issue_halo();
+  issue_w();
+  {
+    [[maybe_unused]] constexpr int sk = 1;
+    dma_wait_barrier<2 * 8>();  // the halo and tap 0 have landed
+    WRES_STAMP(sk);
+    const char* Hs = lds;
 
     floatx4 acc[4][2];
 #pragma unroll
@@ -274,15 +250,10 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
     static_for<0, 18>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       if constexpr (t + 1 < 18) {
-        // one-band workgroups: tap (t + 1) / 2's weight pieces land while taps before it compute
-        if constexpr (NBUF == 1 && (t + 1) % 2 == 0) {
+        // tap (t + 1) / 2's weight pieces land while the taps before it compute
+        if constexpr ((t + 1) % 2 == 0) {
           constexpr int T = (t + 1) / 2;  // the tap that starts here
-          if constexpr (WLA >= 9) {
-            dma_wait_barrier<2 * (8 - T)>();
-          } else {
-            if constexpr (T + WLA - 1 <= 8) issue_wtap(T + WLA - 1);
-            dma_wait_barrier<2 * ((WLA - 1) < (8 - T) ? (WLA - 1) : (8 - T))>();
-          }
+          dma_wait_barrier<2 * (8 - T)>();
         }
         load(t + 1, (t + 1) & 1);
       }
@@ -294,7 +265,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
           acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[t & 1][i], fb[t & 1][jj], acc[i][jj], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
-    if (sk >= 0) WRES_STAMP(sk + 1);
+    WRES_STAMP(sk + 1);
 
     // ---- epilogue through this band's halo buffer (every wave is done reading it).  The
     // residual rows go out first (clamped rows: always-valid addresses, no branch), so their
@@ -319,7 +290,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
 #ifdef SPI_WRES_STAMPS_EPI
     if (sk == 1) WRES_STAMP(4);
 #endif
-    float* T = reinterpret_cast<float*>(lds + BUF * kHBuf);
+    float* T = reinterpret_cast<float*>(lds);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -360,30 +331,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c64_wres(WresArgs a) {
       if (e_ty[it] < rows_left) *reinterpret_cast<half8*>(a.y + (mbase + e_rel[it]) * 64 + e_nb8) = hv[it];
 #endif
     }
-    lds_barrier();  // the tile is read before the next band's halo DMA reuses this buffer
-    if (sk >= 0) WRES_STAMP(sk + 2);
-  };
-
-  issue_halo(b_first, 0);
-  if constexpr (NBUF == 1) {  // one band per workgroup
-    if constexpr (WLA >= 9) {
-      issue_w();
-    } else {
-#pragma unroll
-      for (int tap = 0; tap < WLA; ++tap) issue_wtap(tap);
-    }
-    band_body(std::integral_constant<int, 0>{}, b_first, false, 1);
-    // several bands on one buffer (SPI_CONV_WRES_NBUF=1 with SPI_CONV_WRES_BPW > 1): the weights stay,
-    // each later band's halo goes into the buffer the previous epilogue released (exposed load)
-    for (int j = 1; j < nb; ++j) {
-      issue_halo(b_first + j, 0);
-      band_body(std::integral_constant<int, 0>{}, b_first + j, false, -1, false);
-    }
-  } else {
-    for (int j = 0; j < nb; j += 2) {
-      band_body(std::integral_constant<int, 0>{}, b_first + j, j + 1 < nb, j == 0 ? 1 : -1);
-      if (j + 1 < nb) band_body(std::integral_constant<int, 1>{}, b_first + j + 1, j + 2 < nb, j == 0 ? 4 : -1);
-    }
+    WRES_STAMP(sk + 2);
   }
   WRES_STAMP(7);
 #ifdef SPI_WRES_STAMPS
@@ -396,24 +344,16 @@ int env_int(const char* name, int dflt) {
   return e && *e ? std::atoi(e) : dflt;
 }
 
-// SPI_CONV_WRES=0: never route here; SPI_CONV_WRES_BPW=n: bands per workgroup (0 = rule);
-// SPI_CONV_WRES_NBUF=2: the double-buffered kernel even for one band per workgroup.
-// Read once; conv_wres_reload_env() (spi_debug_gemm_reload_env) re-reads them for sweeps.
-struct WresKnobs {
-  int on = 1, bpw = 0, nbuf = 0, wla = 9;
-};
-WresKnobs read_wres_knobs() {
-  return WresKnobs{env_int("SPI_CONV_WRES", 1), env_int("SPI_CONV_WRES_BPW", 0), env_int("SPI_CONV_WRES_NBUF", 0),
-                   env_int("SPI_CONV_WRES_WLA", 9)};
-}
-WresKnobs& wres_knobs() {
-  static WresKnobs k = read_wres_knobs();
-  return k;
+// SPI_CONV_WRES=0: never route here (A/B runs).  Read once; conv_wres_reload_env()
+// (spi_debug_gemm_reload_env) re-reads it.
+int& wres_on() {
+  static int on = env_int("SPI_CONV_WRES", 1);
+  return on;
 }
 
 }  // namespace
 
-void conv_wres_reload_env() { wres_knobs() = read_wres_knobs(); }
+void conv_wres_reload_env() { wres_on() = env_int("SPI_CONV_WRES", 1); }
 
 #ifdef SPI_WRES_STAMPS
 extern "C" int spi_debug_wres_stamps(unsigned long long* host, size_t n) {
@@ -429,13 +369,13 @@ static int wres_rows(int H, int W) {
 }
 
 bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p) {
-  const int on = wres_knobs().on;
+  const int on = wres_on();
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   return on && prec == Prec::F16 && d.conv && d.KH == 3 && d.KW == 3 && d.stride == 1 && d.pad == 1 &&
          d.Cin == 64 && d.N == 64 && d.K == 576 && d.Kpad == 576 && d.krep == 1 && d.OH == d.H && d.OW == d.W &&
          !d.a_split && !d.out_split && !d.out_f32 && !d.res_f32 && !d.pool_rows && d.ldc == 64 &&
          (!p.res || d.ldr == 64) && d.act != Act::Gelu && wres_rows(d.H, d.W) >= 1 && al16(p.A) && al16(p.W) &&
-         al16(p.C) && (!p.res || al16(p.res)) && p.zeros;
+         al16(p.C) && (!p.res || al16(p.res)) && (!p.bias || al16(p.bias)) && p.zeros && d.w_image;
 }
 
 void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
@@ -454,26 +394,16 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   const int imgs = d.M / (d.OH * d.OW);
   a.bands = imgs * a.bands_per_img;
   const bool relu = d.act == Act::Relu;
-  // bands per workgroup (SPI_CONV_WRES_BPW): 1 keeps the most workgroups in flight (the weights
-  // are re-read from L2 per band), more amortise the 72 KiB weight fill over several bands
-  const int bpw_env = wres_knobs().bpw;
-  int bpw = bpw_env > 0 ? bpw_env : (a.bands >= 512 ? 2 : 1);
-  a.bpw = std::max(1, bpw);
-  const int grid = (a.bands + a.bpw - 1) / a.bpw;
-  // one band per workgroup: one halo buffer (104 KiB of LDS); several bands: the
-  // double-buffered kernel (SPI_CONV_WRES_NBUF=2 forces it for one band too)
-  const bool two = wres_knobs().nbuf == 2 || (a.bpw > 1 && wres_knobs().nbuf != 1);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, s, a); };
-  // SPI_CONV_WRES_WLA=3: weight taps streamed 3 ahead of the computing tap (one-band kind only)
-  const bool la = !two && wres_knobs().wla < 9;
+  const dim3 grid(a.bands);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(NT), 0, s, a); };
   if (a.res && relu)
-    two ? go(conv3x3_c64_wres<true, true, 2>) : la ? go(conv3x3_c64_wres<true, true, 1, 3>) : go(conv3x3_c64_wres<true, true, 1>);
+    go(conv3x3_c64_wres<true, true>);
   else if (a.res)
-    two ? go(conv3x3_c64_wres<true, false, 2>) : la ? go(conv3x3_c64_wres<true, false, 1, 3>) : go(conv3x3_c64_wres<true, false, 1>);
+    go(conv3x3_c64_wres<true, false>);
   else if (relu)
-    two ? go(conv3x3_c64_wres<false, true, 2>) : la ? go(conv3x3_c64_wres<false, true, 1, 3>) : go(conv3x3_c64_wres<false, true, 1>);
+    go(conv3x3_c64_wres<false, true>);
   else
-    two ? go(conv3x3_c64_wres<false, false, 2>) : la ? go(conv3x3_c64_wres<false, false, 1, 3>) : go(conv3x3_c64_wres<false, false, 1>);
+    go(conv3x3_c64_wres<false, false>);
 }
 
 }  // namespace spi

@@ -59,6 +59,25 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
   do {               \
   } while (0)
 #endif
+// Diagnostic build only (-DSPI_GEMM_TIMELINE): four s_memrealtime stamps per
+// workgroup (entry, k-loop start, k-loop end, exit; 100 MHz) and the hardware
+// ids (HW_ID: CU / SE; XCC_ID), so tools/gemm_timeline.py can split a launch
+// into dispatch skew, prologue, loop and epilogue and see how workgroups pack
+// onto CUs.  The real kernel has none of this.
+#ifdef SPI_GEMM_TIMELINE
+__device__ unsigned long long g_gemm_timeline[65536 * 8];
+__device__ int g_gemm_timeline_on;
+#define SPI_RT(v)                                                                  \
+  do {                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+  } while (0)
+#else
+#define SPI_RT(v) \
+  do {            \
+  } while (0)
+#endif
 
 // Diagnostic builds: -DSPI_DIAG_NO_DMA issues no LDS-DMA (the tiles hold stale
 // bytes), -DSPI_DIAG_NO_MFMA reads the fragments but issues no MFMA; timed
@@ -103,17 +122,44 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
 #define SPI_A_SRC(ptr_) (ptr_)
 #endif
 
+// n / d for 0 <= n < 2^31 by one high multiply (host-computed magic, Granlund-Montgomery
+// round-up form: 2^s < d <= 2^(s+1), magic = ceil(2^(32+s) / d) < 2^32, exact since the
+// magic's error (< d) times n stays below 2^(32+s)); d = 1 is magic 0.  The prologue of a
+// launch divides a dozen times (tile decode, output row -> image / row / column), and the
+// compiler's generic 32-bit division is ~40 instructions of dependent SALU / VALU each.
+struct FastDiv {
+  unsigned magic;
+  int shift;
+};
+__host__ __device__ inline FastDiv make_fastdiv(unsigned d) {
+  if (d <= 1) return FastDiv{0u, 0};
+  int s = 0;
+  while ((2ull << s) < d) ++s;  // 2^s < d <= 2^(s+1)
+  return FastDiv{(unsigned)(((1ull << (32 + s)) + d - 1) / d), s};
+}
+__device__ __forceinline__ int fdiv(int n, FastDiv f) {
+  return f.magic ? (int)(__umulhi((unsigned)n, f.magic) >> f.shift) : n;
+}
+
 struct KArgs {
   GemmDesc d;
   GemmPtrs p;
   int k_per_split;  // elements, multiple of the k-step
-  int tiles_m;
+  int tiles_m, tiles_n;
   int tiles;
   int cin_shift;
   int kw_mul;       // ceil(65536 / KW): cell / KW == (cell * kw_mul) >> 16 for cell < 2^12
   int cell_uniform; // conv with Cin >= k-step: one (kh, kw) cell per step
   int vec_ok;       // C / residual rows allow 16-byte vectors of 8 elements (epilogue)
   int xg_m, xg_n;   // XCD rectangles: tile rows in xg_m groups x tile columns in xg_n groups
+  // the rectangles' first tile row per row group (rg_m0[xg_m] = tiles_m) and first tile
+  // column per column group (cg_n0[xg_n] = tile columns), and the row-group heights as
+  // FastDivs: the decode is compares and high multiplies, no loop, no division
+  int rg_m0[9], cg_n0[9];
+  FastDiv fd_rows[8];
+  FastDiv fd_split;      // / splits
+  FastDiv fd_ohw, fd_ow;  // conv: output row m -> image, then row / column
+  FastDiv fd_tiles;       // grouped launches: / tiles
   // halo conv (kConvHalo): tile row block tm is the band of h_th "virtual" output
   // rows u in [tm * h_th, (tm + 1) * h_th) x the full width.  Virtual rows stack the
   // images with a period of h_period rows: image u / h_period, output row
@@ -126,11 +172,6 @@ struct KArgs {
   // blocks, h_bps of them per split-K slice
   int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
   int splits;  // split-K slices (the grid holds tiles x splits workgroups of this problem)
-  // split-K grids: workgroups are decoded so that a tile's slices run on one XCD where the
-  // XCD chunking allows it, and those tiles reduce through that XCD's L2 (plain stores and
-  // loads) instead of write-through slabs (SPI_GEMM_SPLIT_LOCAL=1; measured -10 % fetch on
-  // the layer-3 convs, writes unchanged, four-stream ResNet-18 -1.4 %: off by default)
-  int split_local;
 };
 
 // One launch, one or two independent problems of the same kernel instance (a
@@ -295,28 +336,49 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
   int* s_flag = reinterpret_cast<int*>(lds + LDSB - 16);
+  [[maybe_unused]] unsigned long long rt_e = 0, rt_l0 = 0, rt_l1 = 0, rt_p1 = 0, rt_p2 = 0;
+  SPI_RT(rt_e);
+#ifdef SPI_GEMM_TIMELINE
+  // kind: 0 plain tile, 1 split-K slice that did not reduce, 2 the reducing slice
+  auto tl_out = [&](int kind) {
+    unsigned long long rt_x;
+    SPI_RT(rt_x);
+    if (threadIdx.x == 0 && g_gemm_timeline_on) {
+      unsigned long long* g = g_gemm_timeline + (size_t)((blockIdx.x + blockIdx.y * gridDim.x) & 65535) * 8;
+      g[0] = rt_e;
+      g[1] = rt_l0;
+      g[2] = rt_l1;
+      g[3] = rt_x;
+      g[4] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+             ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+      g[5] = (unsigned long long)kind;
+      g[6] = rt_p1;
+      g[7] = rt_p2;
+    }
+  };
+#else
+  auto tl_out = [](int) {};
+#endif
 
   const GemmDesc& d = a.d;
   // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
+  // hl: the workgroup's dispatch index inside this problem's range; the hardware deals
+  // dispatch indices round-robin to the 8 XCDs, so hl & 7 names the XCD.  Number each
+  // XCD's workgroups consecutively (bijective, chunks of q or q + 1).
   int tile = lin, kslice = kslice_in;
-  [[maybe_unused]] bool xlocal = false;  // this tile's slices all run on one XCD
+  const auto xcd_order = [](int idx, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = idx & 7, l = idx >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+  };
   if (kSplitK<BM, BN, KIND> && a.splits > 1) {
-    // hl: the workgroup's dispatch index inside this problem's range; the hardware deals
-    // dispatch indices round-robin to the 8 XCDs, so hl & 7 names the XCD.  Number each
-    // XCD's workgroups consecutively (bijective, chunks of q or q + 1), then cut that order
-    // into tiles of `splits` consecutive slices: a tile whose slices fall in one chunk is
-    // XCD-local.
-    const int S = a.splits, nwg = a.tiles * S, q = nwg >> 3, r = nwg & 7, x = hl & 7, l = hl >> 3;
-    const int wgid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
-    tile = wgid / S;
-    kslice = wgid - tile * S;
-    const auto chunk = [&](int w) { return w < r * (q + 1) ? w / (q + 1) : r + (w - r * (q + 1)) / max(q, 1); };
-    xlocal = a.split_local && chunk(tile * S) == chunk(tile * S + S - 1);
-  } else {
-    const int nwg = a.tiles, q = nwg >> 3, r = nwg & 7, x = tile & 7, l = tile >> 3;
-    if (nwg >= 16) tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+    // split-K: cut that order into tiles of `splits` consecutive slices
+    const int wgid = xcd_order(hl, a.tiles * a.splits);
+    tile = fdiv(wgid, a.fd_split);
+    kslice = wgid - tile * a.splits;
+  } else if (a.tiles >= 16) {
+    tile = xcd_order(tile, a.tiles);
   }
   // Tile of linear index `tile`: the tile grid is cut into xg_m x xg_n
   // rectangles (row groups i-major), each walked with tm fastest; the chunk of
@@ -325,20 +387,30 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // (xg_m = 1: every XCD reads all of A -- the plain column-major order).
   int tm, tn;
   {
-    const int TM = a.tiles_m, TN = a.tiles / a.tiles_m, gm = a.xg_m, gn = a.xg_n;
-    int i = 0;
-    while (i + 1 < gm && ((i + 1) * TM / gm) * TN <= tile) ++i;
-    const int mlo = i * TM / gm, mi = (i + 1) * TM / gm - mlo;
+    const int TN = a.tiles_n;
+    int mlo = 0, mhi = a.rg_m0[1];
+    FastDiv fdm = a.fd_rows[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i)  // row group: the last whose first tile index is <= tile
+      if (i < a.xg_m && a.rg_m0[i] * TN <= tile) {
+        mlo = a.rg_m0[i];
+        mhi = a.rg_m0[i + 1];
+        fdm = a.fd_rows[i];
+      }
+    const int mi = mhi - mlo;
     const int l2 = tile - mlo * TN;  // index inside row group i: mi x TN tiles
-    const int c = l2 / mi;           // which tile column block it falls in
-    int j = 0;
-    while (j + 1 < gn && (j + 1) * TN / gn <= c) ++j;
-    const int nlo = j * TN / gn;
+    const int c = fdiv(l2, fdm);     // which tile column it falls in
+    int nlo = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+      if (j < a.xg_n && a.cg_n0[j] <= c) nlo = a.cg_n0[j];
     const int loc = l2 - mi * nlo;
-    tm = mlo + loc % mi;
-    tn = nlo + loc / mi;
+    const int lq = fdiv(loc, fdm);
+    tm = mlo + (loc - lq * mi);
+    tn = nlo + lq;
   }
   const int n0 = tn * BN;
+  SPI_RT(rt_p1);
   // m_lim: first row past this tile's valid rows.  Halo tiles map their rows to
   // output rows through the virtual-row bands (halo_m below) instead.
   int m0 = tm * BM, m_lim = d.M;
@@ -395,23 +467,24 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     a_ok[q] = m < d.M;
     const int mm = a_ok[q] ? m : 0;
     if constexpr (CONV) {
-      const int ohw = d.OH * d.OW;
-      const int img = mm / ohw;
-      const int rem = mm - img * ohw;
-      const int oh = rem / d.OW;
+      const int img = fdiv(mm, a.fd_ohw);
+      const int rem = mm - img * (d.OH * d.OW);
+      const int oh = fdiv(rem, a.fd_ow);
       const int ow = rem - oh * d.OW;
       a_ih0[q] = oh * d.stride - d.pad;
       a_iw0[q] = ow * d.stride - d.pad;
       a_base[q] = Ap + (size_t)img * d.H * d.W * d.Cin;
       a_pix[q] = a_base[q] + ((ptrdiff_t)(a_ih0[q] * d.W + a_iw0[q]) << a.cin_shift);
       a_src[q] = a_pix[q] + a_koff[q];
+      // valid taps: kh in [kh_lo, kh_hi) x kw in [kw_lo, kw_hi) -- one row of column bits
+      // replicated per valid filter row (no per-tap compares)
       uint32_t mask = 0u;
-      if (TAP && a_ok[q])
-        for (int kh = 0; kh < d.KH; ++kh)
-          for (int kw = 0; kw < d.KW; ++kw) {
-            const int ih = a_ih0[q] + kh, iw = a_iw0[q] + kw;
-            if ((unsigned)ih < (unsigned)d.H && (unsigned)iw < (unsigned)d.W) mask |= 1u << (kh * d.KW + kw);
-          }
+      if (TAP && a_ok[q]) {
+        const int kh_lo = max(0, -a_ih0[q]), kh_hi = min(d.KH, d.H - a_ih0[q]);
+        const int kw_lo = max(0, -a_iw0[q]), kw_hi = min(d.KW, d.W - a_iw0[q]);
+        const uint32_t cols = kw_hi > kw_lo ? (1u << kw_hi) - (1u << kw_lo) : 0u;
+        for (int kh = kh_lo; kh < kh_hi; ++kh) mask |= cols << (kh * d.KW);
+      }
       a_mask[q] = mask;
     } else {
       a_ih0[q] = a_iw0[q] = 0;
@@ -496,7 +569,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   int cu_cell = 0, cu_kw = 0, cu_ci = 0, cu_off = 0;
   if constexpr (TAP) {
     {
-      const int kbeg_a = kbeg / d.krep;  // A k of the slice's first step (slices hold whole krep groups)
+      const int kbeg_a = d.krep == 2 ? kbeg >> 1 : kbeg;  // A k of the slice's first step (slices hold whole krep groups)
       cu_cell = kbeg_a >> a.cin_shift;
       const int kh = (cu_cell * a.kw_mul) >> 16;
       cu_kw = cu_cell - kh * d.KW;
@@ -590,6 +663,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  SPI_RT(rt_p2);
   if constexpr (HALO) issue_halo(h_b0, 0);  // lands before W step 0 (in-order vmcnt)
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -811,6 +885,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 
   [[maybe_unused]] unsigned long long st_t0 = 0, st_a = 0, st_b = 0, st_c = 0, st_d = 0, st_wait = 0, st_issue = 0, st_comp = 0;
   SPI_STAMP(st_t0);
+  SPI_RT(rt_l0);
   // One k-step; U = t % STAGES is a compile-time constant (the loop below is
   // unrolled by STAGES), so every stage offset -- M0 of the DMAs, the base of
   // the fragment reads -- is an immediate.
@@ -1043,6 +1118,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   }
 
   SPI_STAMP(st_d);
+  SPI_RT(rt_l1);
 #ifdef SPI_GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* gs = g_gemm_stamps + (size_t)(blockIdx.x & 65535) * 8;
@@ -1055,6 +1131,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #endif
   if (!kSplitK<BM, BN, KIND> || a.splits == 1) {
     finish(acc);
+    tl_out(0);
     return;
   }
   if constexpr (kSplitK<BM, BN, KIND>) {
@@ -1069,25 +1146,13 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(tile_slabs, (short)0, splits * SLAB * 4, 0x00020000);
-  // XCD-local tiles: plain stores into this XCD's L2 (written back later, never read back
-  // from memory); others: write-through (sc1) so a reducer on another XCD sees them
-  if (xlocal) {
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 0);
-      }
-  } else {
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
-      }
-  }
+    for (int j = 0; j < TJ; ++j) {
+      const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+    }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   if (tid == 0) {
     const int ticket = __hip_atomic_fetch_add(a.p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1096,7 +1161,10 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     *s_flag = last;
   }
   __syncthreads();
-  if (!*s_flag) return;
+  if (!*s_flag) {
+    tl_out(1);
+    return;
+  }
   // ZR splits' slabs in flight per round (two for the small tiles, one when a
   // slab is 8+ fragments per thread); loads past the last slab fall outside the
   // descriptor's range and return 0 (no branch, no per-load wait).  Slabs are
@@ -1107,32 +1175,17 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // (XCD-local: plain loads from this XCD's L2 -- no L1 line of these slabs can be stale:
-  // the L1 is invalidated at dispatch and only this reducer reads the tile's slabs)
-  const int rd_pol = xlocal ? 0 : 16;
   for (int z0 = 0; z0 < splits; z0 += ZR) {
     floatx4 v[ZR][TI][TJ];
-    if (rd_pol == 0) {
 #pragma unroll
-      for (int zz = 0; zz < ZR; ++zz)
+    for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-            v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-          }
-    } else {
-#pragma unroll
-      for (int zz = 0; zz < ZR; ++zz)
-#pragma unroll
-        for (int i = 0; i < TI; ++i)
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) {
-            const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-            v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-          }
-    }
+        for (int j = 0; j < TJ; ++j) {
+          const int off = ((z0 + zz) * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+          v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+        }
 #pragma unroll
     for (int zz = 0; zz < ZR; ++zz)
 #pragma unroll
@@ -1141,6 +1194,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         for (int j = 0; j < TJ; ++j) sum[i][j] += v[zz][i][j];
   }
   finish(sum);
+  tl_out(2);
   }
 }
 
@@ -1156,7 +1210,7 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
   const bool second = lin >= g.wgs0;
   if (second) lin -= g.wgs0;
   const KArgs& a = second ? g.a[1] : g.a[0];
-  const int kslice = lin / a.tiles;
+  const int kslice = fdiv(lin, a.fd_tiles);
   gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, kslice, lin - kslice * a.tiles, lin);
 }
 
@@ -1175,33 +1229,28 @@ int estep_of(Prec prec) {
 
 // Tuning knobs, read once (getenv on every launch cost ~0.5 us each, and the
 // plan is evaluated three times per launch); spi_debug_gemm_reload_env()
-// re-reads them for in-process sweeps (tools/gemm_bench.py).
-//   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM
-//   SPI_GEMM_POLICY=latency | tput:T      plan rule (default tput:128)
-//   SPI_GEMM_MAXSPLIT=S, SPI_GEMM_STAGES=N  caps for experiments
+// re-reads them for in-process sweeps and tests.  Variants measured and rejected
+// in rounds 1-3 (latency plan rule, 128x64 split-K, 256x128 tiles, 3-stage
+// 128x128 rings, 4-stage halo rings, XCD-local split-K, per-knob ring depths,
+// DESIGN.md 6) are gone; what remains:
+//   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM (sweeps)
+//   SPI_GEMM_POLICY=tput:T               plan target T workgroups (default 128)
+//   SPI_GEMM_MAXSPLIT=S                  cap split-K (1: none)
+//   SPI_GEMM_HALO_CFG                    halo candidates: "0" off, "rows,a|s" forced,
+//                                        "OW:rows,a|s;..." per map width
+//   SPI_GEMM_256_MIN / SPI_GEMM_256_LONGK  gemm256 routing (below)
 struct Knobs {
   bool forced = false;
   Plan plan{};
-  bool latency = false;
   int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
-  int max_split = 0, stages = 0;
+  int max_split = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
-  int halo_stages = 3, halo_minh = 14;
-  int halo_maxtiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles (SPI_GEMM_HALO_MAXTILES)
-  int pair = 1;            // SPI_GEMM_PAIR=0: gemm_pair as two launches
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
   // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
   // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
   // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
   // GEMMs stay off: -1.3 % with them)
   int g256_longk_tiles = 48, g256_longk_k = 1024;
-  int st3_min = 16, st4_min = 32;  // SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN (choose_plan's ring depth; 4 stages from 32
-                                   // k-steps: BERT-base FFN2 four-stream 20.8k -> 21.3k, ViT-L +-0)
-  int sq_stages = 2;       // SPI_GEMM_SQ_STAGES=3: 3-stage ring for dense fp16 128x128 tiles (96 KiB, one workgroup per CU)
-  int dlk_k = 0, dlk_t = 0;  // SPI_GEMM_DENSE_LONGK_T="K,T" (choose_plan)
-  int split128 = 0;        // SPI_GEMM_SPLIT128=1: 128x64 split-K plans (choose_plan)
-  int no_sq128 = 0;        // SPI_GEMM_NO128SQ=1: never 128x128 tiles (128x64 with a 3-stage ring instead)
-  int big = 0;             // SPI_GEMM_BIG=1: 256x128 8-wave tiles for large grids (measured slower)
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
   struct HaloPick {
@@ -1210,10 +1259,12 @@ struct Knobs {
   };
   HaloPick halo_map[8] = {};  // SPI_GEMM_HALO_CFG="OW:rows,a|s;...": per map width
   int n_halo_map = 0;
-  int pair_joint = 2;   // SPI_GEMM_PAIR_JOINT=0: per-problem plans; 1: split-K of a grouped pair sized on both grids; 2: + 128x64 pair tiles when the joint grid allows (launch_pair)
-  int split_local = 0;  // SPI_GEMM_SPLIT_LOCAL=1: XCD-local split-K tiles reduce through L2
-  int xcd2d = 2;  // 2-D tile -> XCD rectangles (xcd_groups); 2: not for split-K grids (plain order there)  // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 };
+// Fixed plan constants (each measured in rounds 1-3):
+constexpr int kHaloStages = 3;     // W ring of the halo kinds
+constexpr int kHaloMinH = 14;      // 7x7 maps: the implicit GEMM measured faster (77 % row use)
+constexpr int kHaloMaxTiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles
+constexpr int kSt3Min = 16, kSt4Min = 32;  // ring depth by k-steps per slice (4 stages: BERT FFN2 +2.4 %)
 
 Knobs read_knobs() {
   Knobs k;
@@ -1228,27 +1279,8 @@ Knobs read_knobs() {
       }
     }
   }
-  if (const char* e = std::getenv("SPI_GEMM_POLICY"); e && *e) {
-    if (std::strcmp(e, "latency") == 0) k.latency = true;
-    if (std::strncmp(e, "tput:", 5) == 0) k.target = std::max(1, std::atoi(e + 5));
-  }
-  if (const char* e = std::getenv("SPI_GEMM_HALO"); e && *e) k.halo = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_XCD2D"); e && *e) k.xcd2d = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_SPLIT_LOCAL"); e && *e) k.split_local = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_HALO_STAGES"); e && *e) k.halo_stages = std::atoi(e) == 4 ? 4 : 3;
-  if (const char* e = std::getenv("SPI_GEMM_HALO_MINH"); e && *e) k.halo_minh = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_HALO_MAXTILES"); e && *e) k.halo_maxtiles = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_PAIR"); e && *e) k.pair = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_PAIR_JOINT"); e && *e) k.pair_joint = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_BIG"); e && *e) k.big = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_ST3_MIN"); e && *e) k.st3_min = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_ST4_MIN"); e && *e) k.st4_min = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_NO128SQ"); e && *e) k.no_sq128 = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_SPLIT128"); e && *e) k.split128 = std::atoi(e);
-  if (const char* e = std::getenv("SPI_GEMM_DENSE_LONGK_T"); e && *e) {
-    if (std::sscanf(e, "%d,%d", &k.dlk_k, &k.dlk_t) != 2 || k.dlk_t < 1) k.dlk_k = 0;
-  }
-  if (const char* e = std::getenv("SPI_GEMM_SQ_STAGES"); e && *e) k.sq_stages = std::atoi(e) == 3 ? 3 : 2;
+  if (const char* e = std::getenv("SPI_GEMM_POLICY"); e && std::strncmp(e, "tput:", 5) == 0)
+    k.target = std::max(1, std::atoi(e + 5));
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_LONGK"); e && *e) {
     int t = 0, kk = 0;
@@ -1260,9 +1292,11 @@ Knobs read_knobs() {
     }
   }
   if (const char* e = std::getenv("SPI_GEMM_HALO_CFG"); e && *e) {
-    // "rows,a|s" for every halo conv, or per map width "OW:rows,a|s;OW:rows,a|s;..."
-    // (OW 0 = any other width; rows 0 = not a halo conv)
-    if (std::strchr(e, ':')) {
+    // "0": no halo kinds; "rows,a|s" for every halo conv, or per map width
+    // "OW:rows,a|s;OW:rows,a|s;..." (OW 0 = any other width; rows 0 = not a halo conv)
+    if (std::strcmp(e, "0") == 0) {
+      k.halo = 0;
+    } else if (std::strchr(e, ':')) {
       for (const char* q = e; q && *q;) {
         int ow = 0, bm = 0;
         char mode = 'a';
@@ -1281,7 +1315,6 @@ Knobs read_knobs() {
     }
   }
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("SPI_GEMM_STAGES"); e && *e) k.stages = std::max(2, std::min(4, std::atoi(e)));
   return k;
 }
 
@@ -1294,8 +1327,7 @@ Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   const Knobs& k = knobs();
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
   if (pl.bn != 64 || (pl.bm != 64 && pl.bm != 128)) pl.splits = 1;  // split-K exists in the 64- and 128-row x 64 kernels only
-  if (k.stages) pl.stages = pl.bm == 128 && pl.bn == 128 ? 2 : pl.bm == 128 ? std::min(k.stages, 3) : k.stages;
-  if (pl.bm == 128) pl.stages = pl.bn == 128 ? k.sq_stages : std::min(pl.stages, 3);  // the instantiated rings
+  if (pl.bm == 128) pl.stages = pl.bn == 128 ? 2 : std::min(pl.stages, 3);  // the instantiated rings
   pl.splits = std::max(1, std::min(pl.splits, ksteps));
   int kt = (ksteps + pl.splits - 1) / pl.splits;
   kt = (kt + krep - 1) / krep * krep;  // krep: slices hold whole (hi, lo) step pairs
@@ -1326,7 +1358,7 @@ Plan halo_candidate(const GemmDesc& d, Prec prec, int T, int bm, bool stacked, i
   if (th == 0) return no;
   const bool small = bm == 64 && (th + 2) * (d.W + 2) <= 3 * 32;  // kConvHaloS
   const int nblk = d.Cin / ES;
-  Plan h{bm, 64, knobs().halo_stages, 1, 0};
+  Plan h{bm, 64, kHaloStages, 1, 0};
   h.nw = nw;
   h.th = th;
   if (stacked) {
@@ -1364,14 +1396,14 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
       return halo_candidate(d, prec, T, hm.bm, hm.stacked, 1 << 20);
     }
   }
-  if (d.OH < knobs().halo_minh) return no;
+  if (d.OH < kHaloMinH) return no;
   // Under the serving load (four worker streams) the implicit GEMM's many small,
   // LDS-light workgroups keep more kernels co-resident than the halo kinds'
   // 56-90 KiB ones: ResNet-18 bs8 59.3k vs 57.0k inf/s, ResNet-152 bs32 10.7k vs
   // 10.0k (tools/policy_sweep.py).  The halo kinds pay where the grid
   // is small and one forward's latency dominates (ResNet-18 bs1: 13.2k vs 12.1k).
   const auto ceil_div = [](int x, int y) { return (x + y - 1) / y; };
-  if (ceil_div(d.M, 64) * ceil_div(d.N, 64) >= knobs().halo_maxtiles) return no;
+  if (ceil_div(d.M, 64) * ceil_div(d.N, 64) >= kHaloMaxTiles) return no;
   const int bm = d.OW > 32 ? 128 : 64;
   return halo_candidate(d, prec, T, bm, false, bm == 64 ? 1 << 20 : 1);  // round 1: only 64-row tiles split
 }
@@ -1383,7 +1415,7 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
 void xcd_groups(const GemmDesc& d, Prec prec, int TM, int TN, int& gm, int& gn) {
   gm = 1;
   gn = std::min(8, TN);
-  if (!knobs().xcd2d || TM * TN < 16) return;
+  if (TM * TN < 16) return;
   const double ea = prec == Prec::F16 ? 2 : 4, ew = prec == Prec::F16 ? 2 : 4;
   const double A = d.conv ? (double)(d.M / (d.OH * d.OW)) * d.H * d.W * d.Cin * ea : (double)d.M * d.K * ea;
   const double W = (double)d.N * d.Kpad * ew;
@@ -1406,61 +1438,28 @@ int plan_tiles(const GemmDesc& d, const Plan& pl) {
   return ((d.M + pl.bm - 1) / pl.bm) * ((d.N + pl.bn - 1) / pl.bn);
 }
 
-// Plan rule (default): the largest tile that still yields >= T workgroups,
-// split-K only when even 64x64 tiles fall short (then to ~T workgroups, >= 6
-// k-steps per slice).  T in 128..192 measured best with 4 concurrent worker
-// streams (ResNet-18 bs8 fp16x3 +8 %, ResNet-152 bs32 +8 %, BERT-base +5 %, ViT-L
-// +7 % over the latency rule; tools/gemm_bench.py / bench.py sweeps);
-// 128 since the joint pair plan (round 3).
-// SPI_GEMM_POLICY=latency keeps the single-stream rule: 64x64 tiles and
-// split-K to ~2 workgroups per CU.
+// Plan rule: the largest tile that still yields >= T workgroups, split-K only
+// when even 64x64 tiles fall short (then to ~T workgroups, >= 6 k-steps per
+// slice).  T in 128..192 measured best with 4 concurrent worker streams
+// (ResNet-18 bs8 fp16x3 +8 %, ResNet-152 bs32 +8 %, BERT-base +5 %, ViT-L +7 %
+// over a single-stream latency rule); 128 since the joint pair
+// plan (round 3).
 Plan choose_plan(const GemmDesc& d, Prec prec) {
   const Knobs& k = knobs();
   const int ES = estep_of(prec);
   const int ksteps = d.Kpad / ES;
   if (k.forced) return finish_plan(k.plan, ksteps, ES, d.krep);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
-  // a deeper ring pays only on long K loops (SPI_GEMM_ST3_MIN / SPI_GEMM_ST4_MIN: the k-steps from
-  // which 3 / 4 stages are used; 4 stages only reach the 64x64 tiles, finish_plan caps the others)
-  const auto stages_for = [&k](int kt) { return kt >= k.st4_min ? 4 : kt >= k.st3_min ? 3 : 2; };
+  // a deeper ring pays only on long K loops (4 stages only reach the 64x64 tiles, finish_plan caps the others)
+  const auto stages_for = [](int kt) { return kt >= kSt4Min ? 4 : kt >= kSt3Min ? 3 : 2; };
   if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);  // one image per tile row
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
-  if (!k.latency) {
-    // SPI_GEMM_DENSE_LONGK_T="K,T": dense GEMMs with Kpad >= K plan for T workgroups (fewer,
-    // larger tiles on long K loops)
-    const int T = (!d.conv && k.dlk_k > 0 && d.Kpad >= k.dlk_k) ? k.dlk_t : k.target;
-    // 256x128 tiles, 8 waves (2 per SIMD), 3 stages: a quarter fewer staging
-    // instructions per MFMA than 128x128 (SPI_GEMM_BIG=1; off by default: ViT-L -4 %, 4096^3 -3 %)
-    if (k.big && d.N > 64 && !d.pool_rows && tiles_of(256, 128) >= T) {
-      Plan p = finish_plan(Plan{256, 128, 3, 1, 0}, ksteps, ES, d.krep);
-      p.nw = 8;
-      p.stages = 3;
-      return p;
-    }
-    if (!k.no_sq128 && d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
-    if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
-    if (k.split128 && ksteps >= 16) {
-      // SPI_GEMM_SPLIT128=1: 128x64 tiles split over K to ~T workgroups (>= 8 k-steps per
-      // slice): a quarter fewer staged bytes per MFMA than 64x64 tiles, fp32 slabs twice as big
-      const int t128 = tiles_of(128, 64);
-      const int sp = std::min((T + t128 - 1) / t128, ksteps / 8);
-      if (sp >= 2) return finish_plan(Plan{128, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
-    }
-    const int t64 = tiles_of(64, 64);
-    const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
-    return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
-  }
-  constexpr int kTarget = 256;  // CUs
-  if (d.N > 64 && tiles_of(128, 128) >= 4 * kTarget) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
-  if (prec == Prec::F16 && tiles_of(128, 64) >= 384 && ksteps >= 32)
-    return finish_plan(Plan{128, 64, 3, 1, 0}, ksteps, ES, d.krep);
-  const int tiles = tiles_of(64, 64);
-  int splits = 1;
-  if (tiles < kTarget) {
-    const int want = (prec == Prec::F16 ? 384 : 512) / tiles;  // workgroups per launch
-    splits = std::max(1, std::min(want, ksteps / 6));            // >= 6 k-steps per slice
-  }
-  return finish_plan(Plan{64, 64, stages_for((ksteps + splits - 1) / splits), splits, 0}, ksteps, ES, d.krep);
+  const int T = k.target;
+  if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
+  if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
+  const int t64 = tiles_of(64, 64);
+  const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
+  return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
 }
 
 int ilog2(int v) {
@@ -1489,13 +1488,25 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   a.p = p;
   a.k_per_split = pl.k_per_split;
   a.splits = pl.splits;
-  a.split_local = knobs().split_local;
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
-  xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, a.tiles_m, a.tiles / a.tiles_m, a.xg_m, a.xg_n);
-  if (pl.splits > 1 && knobs().xcd2d == 2) {  // split-K grids: the plain column-major order
+  const int TM = a.tiles_m, TN = a.tiles / a.tiles_m;
+  a.tiles_n = TN;
+  xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, TM, TN, a.xg_m, a.xg_n);
+  if (pl.splits > 1) {  // split-K grids: the plain column-major order
     a.xg_m = 1;
-    a.xg_n = std::min(8, a.tiles / a.tiles_m);
+    a.xg_n = std::min(8, TN);
+  }
+  for (int i = 0; i <= 8; ++i) {
+    a.rg_m0[i] = std::min(i, a.xg_m) * TM / a.xg_m;
+    a.cg_n0[i] = std::min(i, a.xg_n) * TN / a.xg_n;
+  }
+  for (int i = 0; i < 8; ++i) a.fd_rows[i] = make_fastdiv((unsigned)std::max(1, a.rg_m0[i + 1] - a.rg_m0[i]));
+  a.fd_split = make_fastdiv((unsigned)std::max(1, pl.splits));
+  a.fd_tiles = make_fastdiv((unsigned)std::max(1, a.tiles));
+  if (d.conv) {
+    a.fd_ohw = make_fastdiv((unsigned)(d.OH * d.OW));
+    a.fd_ow = make_fastdiv((unsigned)d.OW);
   }
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
@@ -1521,30 +1532,18 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
   const dim3 grid(g.tiles, pl.splits);
   if (pl.halo) {
     if constexpr (MODE != (int)Prec::F16X3) {  // fp32 A is split at fragment read: not a halo mode
-      if (pl.bm == 256 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 4, kConvHalo, 8>), grid, dim3(512), 0, s, g);
-      else if (pl.bm == 256)
+      if (pl.bm == 256)
         hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, g);
-      else if (pl.bm == 128 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 4, kConvHalo>), grid, dim3(256), 0, s, g);
       else if (pl.bm == 128)
         hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
-      else if (pl.halo == 2 && pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHaloS>), grid, dim3(256), 0, s, g);
       else if (pl.halo == 2)
         hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, g);
-      else if (pl.stages == 4)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 4, kConvHalo>), grid, dim3(256), 0, s, g);
       else
         hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
     }
     return;
   }
-  if (pl.bm == 256)
-    launch_tile<MODE, 256, 128, 3, 8>(g, grid, s);
-  else if (pl.bm == 128 && pl.bn == 128 && pl.stages == 3 && MODE == (int)Prec::F16 && !g.d.conv)
-    hipLaunchKernelGGL((gemm_kernel<MODE, 128, 128, 3, kDense>), grid, dim3(256), 0, s, g);  // SPI_GEMM_SQ_STAGES=3
-  else if (pl.bm == 128 && pl.bn == 128)
+  if (pl.bm == 128 && pl.bn == 128)
     launch_tile<MODE, 128, 128, 2>(g, grid, s);
   else if (pl.bm == 128 && pl.stages == 2)
     launch_tile<MODE, 128, 64, 2>(g, grid, s);
@@ -1591,7 +1590,7 @@ template <int MODE>
 void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, hipStream_t s) {
   const Prec pr = prec_of_mode(MODE);
   Plan q0 = choose_plan(d0, pr), q1 = choose_plan(d1, pr);
-  if (knobs().pair_joint && !q0.halo && !q1.halo && q0.splits > 1 && q0.bm == 64 && q0.bn == 64 &&
+  if (!q0.halo && !q1.halo && q0.splits > 1 && q0.bm == 64 && q0.bn == 64 &&
       q1.bm == 64 && q1.bn == 64) {
     // Joint plan: the grouped launch is one grid, so problem 1's workgroups count
     // toward the T workgroups problem 0's split-K was sized for -- fewer slices,
@@ -1607,9 +1606,9 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
       if (q1.splits == 1) q1.stages = q0.stages;
     }
   }
-  if (knobs().pair_joint >= 2 && !q0.halo && !q1.halo && q0.splits == 1 && q1.splits == 1 && q0.bm == 64 &&
+  if (!q0.halo && !q1.halo && q0.splits == 1 && q1.splits == 1 && q0.bm == 64 &&
       q0.bn == 64 && q1.bm == 64 && q1.bn == 64) {
-    // SPI_GEMM_PAIR_JOINT=2: the largest common tile whose joint grid still reaches T
+    // the largest common tile whose joint grid still reaches T
     // (the layer-2 pair: 98 + 98 tiles of 128 x 64 instead of 196 + 196 of 64 x 64)
     const auto t = [](const GemmDesc& d, int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
     if (t(d0, 128, 64) + t(d1, 128, 64) >= knobs().target) {
@@ -1627,7 +1626,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
     p1s.counters = p0.counters + g.a[0].tiles;
   }
   g.a[1] = make_args<MODE>(d1, p1s, q1);
-  const bool same = knobs().pair && !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
+  const bool same = !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
                     q0.stages == q1.stages && q0.nw == 4 && q1.nw == 4 && g.a[0].cell_uniform &&
                     g.a[1].cell_uniform;
   if (!same) {
@@ -1665,6 +1664,20 @@ extern "C" void spi_debug_gemm_reload_env(void) {
 #ifdef SPI_GEMM_STAMPS
 extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
+#ifdef SPI_GEMM_TIMELINE
+extern "C" int spi_debug_gemm_timeline(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_timeline), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+extern "C" void spi_debug_gemm_timeline_enable(int on, hipStream_t s) {
+  static const int vals[2] = {0, 1};  // stream-ordered: the source must outlive the copy
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gemm_timeline_on), &vals[on ? 1 : 0], sizeof(int), 0,
+                               hipMemcpyHostToDevice, s);
+}
+extern "C" int spi_debug_gemm_timeline_clear(void) {
+  static unsigned long long zeros[65536 * 8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_timeline), zeros, sizeof(zeros)) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -99,8 +99,8 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-// PIPE 1: ping-pong wave rows (default); 0: both wave rows in lock step, two-tile-ahead DMA
-template <int PIPE, int RES>
+// Ping-pong wave rows (the lock-step two-tile-ahead variant measured C5 -2.3 % and was removed, round 4)
+template <int RES>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (PIPE == 1) {
+  {
     // Ping-pong (cdna_hip_programming.md §5, the 256² 8-phase template): every phase is
     //   [reads of its fragments, one quarter's LDS-DMA, counted vmcnt] B_a [MFMAs] B_b
     // and wave row 1 runs one barrier behind wave row 0 (an extra s_barrier up front, one
@@ -238,59 +238,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
     ktile(KT - 1, std::integral_constant<int, 0>{});
     if (wr == 0) bar();  // the skew, closed
-  } else {
-    // Two-tile-ahead staging.  Every k-tile's quarters go out in two groups, Q01 = {Q0, Q1}
-    // and Q23 = {Q2, Q3} (4 DMA instructions per wave each), and tile t + 2's groups are
-    // issued during tile t: Q01(t + 2) at barrier B0(t), once tile t's Q0 / Q1 fragments
-    // (read a phase ahead, at B3(t - 1)) are in registers, and Q23(t + 2) at B3(t), once
-    // Q2(t) / Q3(t) are.  The one-quarter-ahead schedule this replaces kept 16-32 KiB per
-    // CU in flight and gave a quarter two phases to land; at the loaded L2 / MALL latency
-    // (~1 us) that capped the CU at ~14 B/clk of ingest, 2 us per k-tile against the
-    // 0.85 us of MFMAs (Little's law).  Now up to 96 KiB per CU is in flight and a group
-    // has 1.25-1.75 k-tiles to arrive.  The issue order is one sequence Q01(0) Q23(0)
-    // Q01(1) Q23(1) Q01(2) ..., so each wait counts the instructions issued after the
-    // group it needs (vmcnt; see the table in vm_wait); the lgkmcnt(0) in each wait makes
-    // the previous readers of a region done before any wave restages it (WAR).
-    auto stage2 = [&](int g01, int kt) {  // group g01 (0: Q0+Q1, 1: Q2+Q3) of k-tile kt
-      stage(2 * g01, kt);
-      stage(2 * g01 + 1, kt);
-    };
-    stage2(0, 0);
-    stage2(1, 0);
-    if (KT > 1) {
-      stage2(0, 1);
-      stage2(1, 1);
-      vm_wait<12>();
-    } else {
-      vm_wait<4>();
-    }
-    read_a(lds, 0);
-    read_b(lds, 0);
-    // tile t with R = KT - 1 - t tiles after it (R capped at 2): waits before B0 / B1 / B3
-    //   R >= 2: 10 / 12 / 8,  R = 1: 10 / 8 / 4,  R = 0: 2 / 0 / -
-    auto ktile = [&](int kt, auto rem_c) {
-      constexpr int R = decltype(rem_c)::value;
-      const char* buf = lds + (kt & 1) * kBufBytes;
-      vm_wait<R >= 1 ? 10 : 2>();  // B0: Q2(t) landed
-      read_b(buf, 1);
-      if constexpr (R >= 2) stage2(0, kt + 2);
-      mma(0, 0);
-      vm_wait<R >= 2 ? 12 : R == 1 ? 8 : 0>();  // B1: Q3(t) landed
-      read_a(buf, 1);
-      mma(0, 1);
-      mma(1, 0);
-      if constexpr (R >= 1) {
-        vm_wait<R >= 2 ? 8 : 4>();  // B3: Q0(t + 1), Q1(t + 1) landed
-        const char* nbuf = lds + ((kt + 1) & 1) * kBufBytes;
-        read_a(nbuf, 0);
-        read_b(nbuf, 0);
-        if constexpr (R >= 2) stage2(1, kt + 2);
-      }
-      mma(1, 1);
-    };
-    for (int kt = 0; kt < KT - 2; ++kt) ktile(kt, std::integral_constant<int, 2>{});
-    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
-    ktile(KT - 1, std::integral_constant<int, 0>{});
   }
 
   // Epilogue through LDS (the k-loop's buffers are free): per-element stores from the
@@ -337,7 +284,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     return;
   }
   // The walk is branch-free per row: the residual kind (none / fp16 / fp32) is a template
-  // parameter and rows past M load a clamped, valid row (and store duplicates, below).  A runtime
+  // parameter and rows past M load a clamped, valid row; in the last tile row (GUARD) their
+  // stores are skipped -- never store the duplicates: with C the residual buffer (in place,
+  // ViT's residual stream) a duplicate raced with the real row (fixed in round 3).  A runtime
   // `if (res)` or a guarded bias load per element had hipcc branch around each load and wait
   // vmcnt(0) per row (the weight-resident conv measured that as 40 % of its epilogue).  Each
   // thread's 8 residual rows of a round are loaded before the round's park, so their latency
@@ -491,16 +440,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 
 }  // namespace
 
-static int g_pipe = -1;
-static int g256_pipe() {
-  if (g_pipe < 0) {
-    const char* e = std::getenv("SPI_G256_PIPE");  // 1 ping-pong wave rows (default), 0 lock step
-    g_pipe = e && *e ? std::atoi(e) : 1;
-  }
-  return g_pipe;
-}
-
-void gemm256_reload_env() { g_pipe = -1; }
+void gemm256_reload_env() {}
 
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles) {
   if (min_tiles <= 0 || prec != Prec::F16 || d.conv || d.krep != 1 || d.a_split || d.out_split || d.pool_rows ||
@@ -535,21 +475,12 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
                  ? 1 : 0;
   const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
   const dim3 grid(g.tiles_m * g.tiles_n), blk(512);
-  if (g256_pipe() == 1) {
-    if (res == 0)
-      hipLaunchKernelGGL((gemm256_kernel<1, 0>), grid, blk, 0, s, g);
-    else if (res == 1)
-      hipLaunchKernelGGL((gemm256_kernel<1, 1>), grid, blk, 0, s, g);
-    else
-      hipLaunchKernelGGL((gemm256_kernel<1, 2>), grid, blk, 0, s, g);
-  } else {
-    if (res == 0)
-      hipLaunchKernelGGL((gemm256_kernel<0, 0>), grid, blk, 0, s, g);
-    else if (res == 1)
-      hipLaunchKernelGGL((gemm256_kernel<0, 1>), grid, blk, 0, s, g);
-    else
-      hipLaunchKernelGGL((gemm256_kernel<0, 2>), grid, blk, 0, s, g);
-  }
+  if (res == 0)
+    hipLaunchKernelGGL((gemm256_kernel<0>), grid, blk, 0, s, g);
+  else if (res == 1)
+    hipLaunchKernelGGL((gemm256_kernel<1>), grid, blk, 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<2>), grid, blk, 0, s, g);
 }
 
 }  // namespace spi

@@ -200,6 +200,7 @@ ConvW pack_conv(const PMap& p, const std::string& wname, const std::string& bn, 
     });
   } else {
     c.w = pack_matrix(c.cout, K, c.npad, c.kpad, prec, folded);
+    c.w_image = packed_has_wres_image(prec, c.cout, K, c.npad, c.kpad);
   }
   c.wplane = (size_t)c.npad * c.kpad;
   c.b = pack_vec(f.b.data(), c.cout);
@@ -452,7 +453,6 @@ void Model::build_resnet(const PMap& p) {
   const int stem_ow = (image_ + 6 - 7) / 2 + 1;
   stem_fused_ = !(fe && *fe && std::atoi(fe) == 0) && stem_.cout == 64 && stem_.stride == 2 &&
                 stem_ow <= kStemPoolMaxOW && (prec_ == Prec::F16 || split_);
-  if (const char* e = std::getenv("SPI_STEM_PR"); e && *e) stem_pr_ = std::atoi(e);  // 1 / 2: 4-wave variants
   if (stem_fused_) {
     std::vector<_Float16> packed(stem_pool_bytes() / sizeof(_Float16));
     stem_pool_pack(stem_folded.w.data(), packed.data());
@@ -662,6 +662,7 @@ GemmDesc conv_desc(const ConvW& c, int B, int H, int W, int& OH, int& OW) {
   d.stride = c.stride;
   d.pad = c.pad;
   d.krep = c.krep;
+  d.w_image = c.w_image;
   return d;
 }
 
@@ -1159,12 +1160,18 @@ namespace spi {
 
 thread_local std::vector<Model::OpRecord>* Model::prof_ = nullptr;
 thread_local Model::ProfRepeat* Model::prof_rep_ = nullptr;
+#ifdef SPI_GEMM_TIMELINE
+extern "C" void spi_debug_gemm_timeline_enable(int on, hipStream_t s);
+#endif
 
 int Model::op_begin(hipStream_t s, const std::string& name, double flops, double bytes) {
   OpRecord r{name, flops, bytes, nullptr, nullptr, 1};
   if (prof_rep_ && !prof_rep_->done && name == prof_rep_->name) {  // the op profile_op() repeats
     prof_rep_->done = true;
     r.reps = prof_rep_->reps;
+#ifdef SPI_GEMM_TIMELINE
+    spi_debug_gemm_timeline_enable(1, s);  // stamp only the repeated op's launches
+#endif
   }
   SPI_HIP(hipEventCreate(&r.start));
   SPI_HIP(hipEventCreate(&r.stop));
@@ -1173,7 +1180,12 @@ int Model::op_begin(hipStream_t s, const std::string& name, double flops, double
   return r.reps;
 }
 
-void Model::op_end(hipStream_t s) { SPI_HIP(hipEventRecord(prof_->back().stop, s)); }
+void Model::op_end(hipStream_t s) {
+  SPI_HIP(hipEventRecord(prof_->back().stop, s));
+#ifdef SPI_GEMM_TIMELINE
+  if (prof_->back().reps > 1) spi_debug_gemm_timeline_enable(0, s);
+#endif
+}
 
 int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* const* out, float* ms,
                    double* flops, double* bytes, char* names, int name_len, int max_ops) {

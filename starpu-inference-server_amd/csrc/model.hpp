@@ -26,6 +26,7 @@ struct ConvW {
   size_t wplane = 0;
   Prec prec = Prec::F16;  // packing / contraction precision of this conv
   int krep = 1;           // 2: hi + lo weight steps per A step (GemmDesc::krep; SPI_PREC_F16M)
+  bool w_image = false;   // the packed rows 64..127 hold conv_wres's LDS image (GemmDesc::w_image)
 };
 
 struct LinearW {

@@ -132,6 +132,8 @@ int spi_op_conv2d(int32_t precision, const void* x, int32_t B, int32_t H, int32_
   d.ldc = Cout;
   d.ldr = Cout;
   d.act = static_cast<spi::Act>(act);
+  // W_packed comes from spi_op_pack_weight (spi_ops.h), which writes the image rows
+  d.w_image = spi::packed_has_wres_image(p, Cout, d.K, spi::round_up_to(Cout, 128), d.Kpad);
   if (precision == kSplitPrecision) {
     if (Cin < 32 || Cout % 32 || KH * KW > 31)
       return fail("split conv needs Cin >= 32, Cout a multiple of 32 and <= 31 filter taps");

@@ -13,6 +13,13 @@ inline size_t packed_bytes(Prec prec, int Npad, int Kpad) {
   return (size_t)Npad * Kpad * (prec == Prec::F16 ? 2 : 4);
 }
 
+// Whether pack_matrix_into writes the weight-resident conv's LDS image into the padding
+// rows (below): exactly the fp16 64 x 576 matrices.  A GemmDesc whose W came from such a
+// pack says so with GemmDesc::w_image, and only then may conv_wres read those rows.
+inline bool packed_has_wres_image(Prec prec, int N, int K, int Npad, int Kpad) {
+  return prec == Prec::F16 && N == 64 && K == 576 && Npad == 128 && Kpad == 576;
+}
+
 // [N][K] -> [Npad][Kpad] in the compute layout; get(n, k) returns element (n, k).
 // F16X3 rows are Kpad/32 blocks of [32 hi fp16 | 32 lo fp16] (lo = v - hi).
 template <typename F>
@@ -37,7 +44,7 @@ void pack_matrix_into(char* dst, int N, int K, int Npad, int Kpad, Prec prec, F 
   // they hold the weight-resident conv's LDS image instead (conv_wres.hip) -- per tap t,
   // row n, 16-byte slot s: chunk s ^ (n & 7) of W[n][t * 64 ...] -- so that kernel fills
   // its LDS with 72 contiguous 1-KiB pieces.
-  if (prec == Prec::F16 && N == 64 && K == 576 && Npad == 128 && Kpad == 576) {
+  if (packed_has_wres_image(prec, N, K, Npad, Kpad)) {
     const _Float16* w = reinterpret_cast<const _Float16*>(dst);
     _Float16* img = reinterpret_cast<_Float16*>(dst) + (size_t)64 * Kpad;
     for (int t = 0; t < 9; ++t)

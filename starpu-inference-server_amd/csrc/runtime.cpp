@@ -393,6 +393,7 @@ struct spi_runtime {
   bool congested = false;      // a submission was rejected since the last decision
   spi_batching_state bstate{};
   int32_t last_target = 0;
+  double warmup_s = 0.0;  // spi_runtime_create's per-worker warm-up
   std::atomic<int64_t> completed{0}, failed{0};
 
   void run(Worker* w);
@@ -980,6 +981,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     for (int b = 1; b <= upto; ++b) warm.push_back(b);
   }
   if (warm.empty() || warm.back() != cfg.max_batch) warm.push_back(cfg.max_batch);
+  const auto warm_t0 = std::chrono::steady_clock::now();
   for (auto& w : rt->workers) {
     (void)hipSetDevice(w->device);
     for (int b : warm)
@@ -987,6 +989,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
         return cleanup_fail(std::string("warm-up failed for worker ") + std::to_string(w->worker_id) + " batch " +
                             std::to_string(b) + ": " + spi_last_error());
   }
+  rt->warmup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - warm_t0).count();
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
   if (const char* e = std::getenv("SPI_H2D_SDMA_WAIT"); e && std::strcmp(e, "blocked") == 0) rt->sdma_wait_blocked = true;
   if (const char* e = std::getenv("SPI_RT_COMPLETION"); e && std::strcmp(e, "spin") == 0) rt->spin_completion = true;
@@ -1072,6 +1075,8 @@ int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out
 }
 
 int32_t spi_runtime_h2d_mode(const spi_runtime* rt) { return rt ? rt->cfg.h2d_mode : -1; }
+
+double spi_runtime_warmup_seconds(const spi_runtime* rt) { return rt ? rt->warmup_s : 0.0; }
 
 int32_t spi_runtime_batch_target(const spi_runtime* rt) {
   if (!rt) return 0;

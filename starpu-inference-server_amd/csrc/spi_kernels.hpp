@@ -52,6 +52,9 @@ struct GemmDesc {
   // staged twice, so one launch accumulates x.w_hi + x.w_lo (~22-bit weights on fp16 MFMAs).
   // Kpad is the packed (W) row length; K stays the logical A length.
   int krep = 1;
+  // W came from pack_matrix_into of an fp16 64 x 576 matrix, whose padding rows 64..127
+  // hold the weight-resident conv's LDS image (pack.hpp); conv_wres requires it.
+  bool w_image = false;
 };
 
 struct GemmPtrs {

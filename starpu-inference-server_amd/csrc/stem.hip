@@ -296,10 +296,12 @@ __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restr
 template <int PR, int NW>
 void launch_pr(const float* x, const _Float16* w, const float* bias, void* y, int B, int H, int W, int OH, int OW,
                int PH, int PW, bool lo, bool split, hipStream_t s) {
-  static const int diag = [] {
-    const char* e = std::getenv("SPI_STEM_DIAG");  // 1: no image loads, 2: fill only, 3: empty
-    return e && *e ? std::atoi(e) : 0;
-  }();
+  // diagnostic builds only (-DSPI_STEM_DIAG=1: no image loads, 2: fill only, 3: empty)
+#ifdef SPI_STEM_DIAG
+  constexpr int diag = SPI_STEM_DIAG;
+#else
+  constexpr int diag = 0;
+#endif
   const dim3 grid((PH + PR - 1) / PR, B), block(64 * NW);
   if (split)
     hipLaunchKernelGGL((stem_pool_kernel<PR, NW, true, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);

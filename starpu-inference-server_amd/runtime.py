@@ -115,6 +115,7 @@ for _name, _res, _args in [
     ("spi_runtime_num_workers", C.c_int32, [C.c_void_p]),
     ("spi_runtime_worker_times", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
     ("spi_runtime_batch_target", C.c_int32, [C.c_void_p]),
+    ("spi_runtime_warmup_seconds", C.c_double, [C.c_void_p]),
     ("spi_runtime_h2d_mode", C.c_int32, [C.c_void_p]),
     ("spi_runtime_destroy", None, [C.c_void_p]),
     ("spi_runtime_loadgen", C.c_int, [C.c_void_p, C.POINTER(LoadgenConfig), C.POINTER(C.c_void_p),
@@ -249,6 +250,11 @@ class Runtime:
     @property
     def batch_target(self) -> int:
         return lib.spi_runtime_batch_target(self.handle)
+
+    @property
+    def warmup_seconds(self) -> float:
+        """Wall time of the per-worker warm-up at create (graph captures, workspaces)."""
+        return lib.spi_runtime_warmup_seconds(self.handle)
 
     def _done(self, _user, request_id, status, error, t):
         tt = t.contents

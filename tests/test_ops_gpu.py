@@ -258,42 +258,6 @@ def test_conv_halo_candidates_fp16(ops, halo_cfg, cfg, B, H, cin, cout):
     assert err < 2e-3, f"fp16 halo {cfg} conv {B}x{H}x{cin}->{cout}: {err:.3e}"
 
 
-@pytest.fixture
-def big_tiles(ops):
-    import os
-    os.environ["SPI_GEMM_BIG"] = "1"
-    ops.lib.spi_debug_gemm_reload_env()
-    yield
-    os.environ.pop("SPI_GEMM_BIG", None)
-    ops.lib.spi_debug_gemm_reload_env()
-
-
-@pytest.mark.parametrize("prec", PRECS + ["fp16x3s"])
-@pytest.mark.parametrize("M,N,K", [(3152, 3072, 1024), (6144, 1000, 256)])
-def test_gemm_256x128_eight_waves(ops, big_tiles, prec, M, N, K):
-    """The opt-in 256x128 / 8-wave tiles (SPI_GEMM_BIG=1) on grids large enough to take them."""
-    g = torch.Generator().manual_seed(M + 3 * N + K)
-    A = torch.randn(M, K, generator=g)
-    W = torch.randn(N, K, generator=g) / K ** 0.5
-    b = torch.randn(N, generator=g)
-    if prec == "fp16x3s":
-        if N % 32:
-            pytest.skip("the split layout needs N a multiple of 32")
-        As = ops.to_split(A)
-        ref = ops.from_split(As) @ W.T + b
-        out = ops.gemm(prec, As.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda(),
-                       out=torch.empty(M, N, device="cuda"))
-        err = normalized_max_error(ops.from_split(out.cpu()).numpy(), ref.numpy())
-        assert err < 1e-5
-        return
-    dt = ops.act_dtype(prec)
-    A_in = A.to(dt)
-    ref = A_in.float() @ (W.half().float() if prec == "fp16" else W).T + b
-    out = ops.gemm(prec, A_in.cuda(), ops.pack_weight(prec, W), N, bias=b.cuda())
-    err = normalized_max_error(out.cpu().numpy(), ref.numpy())
-    assert err < TOL[prec], f"{prec} {M}x{N}x{K}: {err:.3e}"
-
-
 def stem_pool_ref(x, w, b):
     """torchvision's conv1 (BN folded into w / b) + relu + maxpool, fp32."""
     return F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1).permute(0, 2, 3, 1)
@@ -404,13 +368,14 @@ def test_gemm256_unaligned_output(ops, gemm256_everywhere):
     assert normalized_max_error(out.float().cpu().numpy(), ref.numpy()) < 2e-3
 
 
-@pytest.mark.parametrize("B,H", [(8, 56), (1, 56), (3, 16), (2, 13), (2, 40), (5, 28), (1, 61)])
+@pytest.mark.parametrize("B,H", [(8, 56), (1, 56), (3, 16), (2, 13), (2, 40), (5, 28), (1, 61), (32, 56), (19, 56)])
 @pytest.mark.parametrize("res,act,bias", [(True, "relu", True), (False, "relu", True), (True, None, True),
                                           (False, None, False)])
 def test_conv3x3_c64_weight_resident(ops, B, H, res, act, bias):
     """The weight-resident 64 -> 64 3x3 conv (conv_wres.hip, ResNet layer 1): bands of 2 rows at
-    56 wide, 8 at 16 wide, partial last bands (13, 61), with / without the residual and ReLU,
-    against an fp32 conv of the fp16-rounded operands."""
+    56 wide, 8 at 16 wide, partial last bands (13, 61), ResNet-152's bs32 grid (896 bands) and an
+    odd band count (19 x 28), with / without the residual and ReLU, against an fp32 conv of the
+    fp16-rounded operands."""
     g = torch.Generator().manual_seed(B * 100 + H)
     x = torch.rand(B, H, H, 64, generator=g).half()
     w = torch.randn(64, 64, 3, 3, generator=g) * (2.0 / 576) ** 0.5
