@@ -234,23 +234,45 @@ def committed_rocprof(op):
     return None
 
 
+def trace_ranking(model, batch, precision):
+    """The committed rocprofv3 kernel trace of this config's graph-replayed timed loop, regrouped
+    per op (profiles/<round>/trace_<model>_bs<B>_<prec>_ops.csv, tools/trace_round.sh +
+    tools/trace_ops.py --launches): rows largest total device time first, and the file."""
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"trace_{model}_bs{batch}_{precision}_ops.csv")))
+    if not hits:
+        return [], None
+    import csv
+    with open(hits[-1]) as f:
+        rows = [r for r in csv.DictReader(f) if r.get("op")]
+    rows.sort(key=lambda r: -float(r["total_us"]))
+    return rows, os.path.relpath(hits[-1], ROOT)
+
+
 def roofline(h, precision, model, reps=200, name=None):
-    """The dominant op under the four-stream load (largest device time per forward; `name`
-    overrides the choice), and its roofline: algorithmic FLOPs (or bytes) per launch over its
-    steady-state launch duration -- `reps` launches of that op back to back on worker 0's
-    stream between one pair of hipEvents (Model::profile_op), the same launches a rocprofv3
-    kernel trace of `bench.py --roofline-only --roofline-op NAME` counts (profiles/<round>/).
-    The per-launch event times under the four-stream load are reported beside it."""
+    """The op that bounds the timed loop, and its roofline: algorithmic FLOPs (or bytes) per
+    launch over its steady-state launch duration -- `reps` launches of that op back to back on
+    worker 0's stream between one pair of hipEvents (Model::profile_op), the same launches a
+    rocprofv3 kernel trace of `bench.py --roofline-only --roofline-op NAME` counts.
+    Which op: the largest summed device time in the committed rocprofv3 trace of this config's
+    graph-replayed timed loop (trace_ranking); without one, the largest device time per
+    forward of an eager forward under the four-stream load.  `name` overrides the choice.  The
+    per-launch event times under the four-stream load are reported beside it."""
+    ranking, rsrc = trace_ranking(model, h.batch, precision)
     loaded = h.op_profile(True) if name is None else None
-    if name is None:
+    selection = "given"
+    if name is None and ranking:
+        name = ranking[0]["op"].split("|")[0]
+        selection = f"largest summed device time in the rocprofv3 trace of the graph-replayed timed loop ({rsrc})"
+    elif name is None:
         name = max(loaded.items(), key=lambda kv: kv[1][0])[0]
+        selection = "largest device time per forward, eager forward under the four-stream load (no committed trace)"
     micro = h.replica.profile_op(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream, name, reps)
     ms, flops, nbytes = micro["ms"], micro["flops"], micro["bytes"]
     peak = PEAK_TFLOPS[precision]
     traffic, tsrc = committed_profile("traffic", model, h.batch, precision)
     mfma, msrc = committed_profile("mfma", model, h.batch, precision)
     t_bytes = traffic.get(name, {}).get("hbm_bytes_per_launch")
-    common = {"kernel": name, "avg_launch_ms": round(ms, 5), "reps": reps,
+    common = {"kernel": name, "selection": selection, "avg_launch_ms": round(ms, 5), "reps": reps,
               "measured": f"hipEvents around {reps} back-to-back launches of the op on its stream "
                           "(Model::profile_op); rocprofv3 summary of the same launches in profiles/",
               "traffic": t_bytes, "traffic_source": tsrc,
@@ -262,7 +284,16 @@ def roofline(h, precision, model, reps=200, name=None):
         common["frac_rocprof"] = round((flops / (rp["avg_ms"] * 1e-3) / 1e12 / peak) if flops else
                                        (nbytes / (rp["avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS), 5)
         common["rocprof_source"] = rp["source"]
-    if loaded is not None:
+    tr = next((r for r in ranking if name in r["op"].split("|")), None)
+    if tr is not None:  # the same op in the timed loop's trace (profiler-perturbed concurrency)
+        common["timed_loop_trace"] = {
+            "share_of_device_time": float(tr["share"]), "mean_us": float(tr["mean_us"]),
+            "median_us": float(tr["median_us"]), "kernel": tr["kernel"],
+            "grid": [int(tr["workgroups_x"]), int(tr["grid_y"])],
+            "frac_at_trace_mean": round((flops / (float(tr["mean_us"]) * 1e-6) / 1e12 / peak) if flops else
+                                        (nbytes / (float(tr["mean_us"]) * 1e-6) / 1e9 / PEAK_HBM_GBS), 5),
+            "source": rsrc}
+    if loaded is not None and name in loaded:
         tot, cnt = loaded[name][0], loaded[name][1]
         fwd_loaded = sum(v[0] for v in loaded.values())
         ms_l = tot / max(cnt, 1)
@@ -479,6 +510,10 @@ def main():
                     help="only the dominant op's back-to-back launches (the rocprofv3 roofline command)")
     ap.add_argument("--roofline-op", default="", help="op name for --roofline-only (default: chosen under load)")
     ap.add_argument("--roofline-reps", type=int, default=200)
+    ap.add_argument("--loop-only", action="store_true",
+                    help="only the timed loop (the rocprofv3 trace command of tools/trace_round.sh)")
+    ap.add_argument("--launch-table", default="",
+                    help="write one eager forward's kernel launches (op, kernel, grid) here as TSV (rank 0)")
     ap.add_argument("--control-plane-only", action="store_true",
                     help="test hook (tests/test_host.py): run the multi-rank control path -- rank spawn, gloo "
                          "rendezvous, barrier + max-over-ranks timing, e2e aggregation, the JSON line -- around "
@@ -523,6 +558,19 @@ def main():
     replica = spi.ModelReplica(model, dev, args.precision, max_batch=args.batch,
                                seq_len=seq if args.model.startswith("bert") else 0, graphs=bool(args.graphs))
     h = Harness(spi, replica, args.model, dev, args.batch, args.workers, np.random.default_rng(rank))
+    if args.launch_table and rank == 0:
+        with open(args.launch_table, "w") as f:
+            for r in replica.launch_table(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream):
+                f.write("\t".join(str(x) for x in (r["op_index"], r["op"], r["kernel"], *r["grid"], r["block"])) + "\n")
+        torch.cuda.synchronize(dev)
+    if args.loop_only:
+        elapsed = h.throughput(args.steps, args.warmup, args.tasks_per_step, world, dist)
+        per_step = args.workers * args.tasks_per_step * args.batch
+        if rank == 0:
+            print(json.dumps({"loop_only": True, "model": args.model, "batch": args.batch, "dtype": args.precision,
+                              "value": round(world * per_step * args.steps / elapsed, 2),
+                              "ms_per_step": round(elapsed * 1e3 / args.steps, 4)}), flush=True)
+        return
     if args.roofline_only:
         h.rounds(1)
         torch.cuda.synchronize(dev)
@@ -578,6 +626,15 @@ def main():
         result["model_gflop_per_inference"] = round(replica.flops(1) / 1e9, 4)
         result["model_tflops_per_gpu"] = round(replica.flops(1) * value / world / 1e12, 3)
         result["roofline"] = roofline(h, args.precision, args.model, args.roofline_reps)
+        # the next ops of the timed loop's trace, each timed the same way (e.g. the layer-1 conv)
+        ranking, _ = trace_ranking(args.model, args.batch, args.precision)
+        nxt = []
+        for r in ranking[1:3]:
+            rl = roofline(h, args.precision, args.model, args.roofline_reps, name=r["op"].split("|")[0])
+            nxt.append({k: rl[k] for k in ("kernel", "avg_launch_ms", "achieved", "frac") if k in rl} |
+                       {"share_of_device_time": float(r["share"])})
+        if nxt:
+            result["roofline_next_ops"] = nxt
     # submit -> outputs in host memory, incl. H2D and D2H, through the runtime
     # closed loop on every rank's GPU, 8 requests in flight per worker (the H2D link -- 51 GB/s
     # measured, 85k inf/s of fp32 NCHW bs8 input -- and the compute pipeline both stay busy), and
@@ -621,6 +678,9 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        # the serving figures last, so a tail of the line still carries them
+        result["e2e"] = result.pop("e2e")
+        result["e2e_summary"] = {k: result["e2e"][k] for k in ("value", "p50_latency_ms", "p99_latency_ms")}
         print(json.dumps(result), flush=True)
 
 

@@ -293,6 +293,13 @@ int spi_model_profile(spi_model* model, void* stream, int64_t batch, int64_t seq
 int spi_model_profile_op(spi_model* model, void* stream, int64_t batch, int64_t seq,
                          const void* const* inputs, void* const* outputs, const char* op_name,
                          int32_t reps, float* ms_per_launch, double* flops, double* bytes);
+/* Measurement hook: one eager forward on `stream` with every kernel launch recorded,
+ * as text, one line per launch: "op_index\top_name\tkernel\tgrid_x\tgrid_y\tgrid_z\tblock\n"
+ * (grid in workgroups).  It maps a rocprofv3 kernel trace of graph-replayed forwards,
+ * which names kernels and grids only, back to ops (tools/trace_ops.py --launches).
+ * Writes at most buflen - 1 bytes plus a NUL; returns the full length, or -1 on error. */
+int64_t spi_model_launch_table(spi_model* model, void* stream, int64_t batch, int64_t seq,
+                               const void* const* inputs, void* const* outputs, char* buf, size_t buflen);
 /* Capture launch-bound forwards into hipGraphs (per stream, per batch). */
 void spi_model_set_graphs(spi_model* model, int32_t enable);
 /* Per-worker warm-up (inference_runner.cpp:507-560): allocate `stream`'s

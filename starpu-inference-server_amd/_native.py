@@ -184,6 +184,8 @@ _PROTOS = {
     "spi_model_profile_op": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_void_p),
                                        C.POINTER(C.c_void_p), C.c_char_p, C.c_int32, C.POINTER(C.c_float),
                                        C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "spi_model_launch_table": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_void_p), C.c_char_p, C.c_size_t]),
     "spi_device_count": (C.c_int, []),
     "spi_set_device": (C.c_int, [C.c_int32]),
     "spi_device_malloc": (C.c_void_p, [C.c_size_t]),

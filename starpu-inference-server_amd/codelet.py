@@ -234,6 +234,29 @@ class ModelReplica:
         return [dict(name=raw[i * name_len:(i + 1) * name_len].split(b"\0")[0].decode(), ms=ms[i], flops=fl[i],
                      bytes=by[i]) for i in range(n)]
 
+    def launch_table(self, inputs: Sequence[torch.Tensor], out: torch.Tensor, stream: int) -> list[dict]:
+        """One eager forward with every kernel launch recorded (measurement only): per launch its
+        op (index, name), kernel (template id) and grid in workgroups."""
+        ins = (C.c_void_p * max(1, len(inputs)))(*[x.data_ptr() for x in inputs])
+        outs = (C.c_void_p * 1)(out.data_ptr())
+        seq = int(inputs[0].shape[1]) if inputs[0].dim() >= 2 else 0
+        size = 1 << 20
+        while True:
+            buf = C.create_string_buffer(size)
+            n = lib.spi_model_launch_table(self.handle, C.c_void_p(stream), int(inputs[0].shape[0]), seq, ins, outs,
+                                           buf, size)
+            if n < 0:
+                raise InferenceExecutionException(f"launch_table failed: {N.last_error()}")
+            if n < size:
+                break
+            size = int(n) + 1
+        rows = []
+        for line in buf.value.decode().splitlines():
+            i, name, kernel, gx, gy, gz, block = line.split("\t")
+            rows.append(dict(op_index=int(i), op=name, kernel=kernel, grid=(int(gx), int(gy), int(gz)),
+                             block=int(block)))
+        return rows
+
     def profile_op(self, inputs: Sequence[torch.Tensor], out: torch.Tensor, stream: int, name: str,
                    reps: int = 200) -> dict:
         """One eager forward with op `name` launched `reps` times back to back between one pair

@@ -378,13 +378,13 @@ void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S,
   const dim3 grid((S + QT - 1) / QT, B * heads);
   if (f16 && S > 128) {
     const dim3 g8((S + 127) / 128, B * heads);
-    hipLaunchKernelGGL(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
+    SPI_LAUNCH(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
   } else if (f16) {
-    hipLaunchKernelGGL(attn_f16_swapped_kernel<4>, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
+    SPI_LAUNCH(attn_f16_swapped_kernel<4>, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
   } else {
-    hipLaunchKernelGGL((attn_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv,
+    SPI_LAUNCH((attn_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv,
                        mask_bias, (float*)ctx, S, heads, scale);
   }
 }

@@ -386,6 +386,20 @@ int spi_model_profile_op(spi_model* m, void* stream, int64_t batch, int64_t seq,
   }
 }
 
+int64_t spi_model_launch_table(spi_model* m, void* stream, int64_t batch, int64_t seq, const void* const* inputs,
+                               void* const* outputs, char* buf, size_t buflen) {
+  if (!m) return -1;
+  try {
+    const std::string t =
+        m->impl->launch_table(static_cast<hipStream_t>(stream), (int)batch, (int)seq, inputs, outputs);
+    if (buf && buflen > 0) std::snprintf(buf, buflen, "%s", t.c_str());
+    return (int64_t)t.size();
+  } catch (const std::exception& e) {
+    tl_last_error = e.what();
+    return -1;
+  }
+}
+
 void spi_model_set_graphs(spi_model* m, int32_t on) {
   if (m) m->impl->set_graphs(on != 0);
 }

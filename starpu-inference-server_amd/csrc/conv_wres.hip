@@ -395,15 +395,14 @@ void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   a.bands = imgs * a.bands_per_img;
   const bool relu = d.act == Act::Relu;
   const dim3 grid(a.bands);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(NT), 0, s, a); };
   if (a.res && relu)
-    go(conv3x3_c64_wres<true, true>);
+    SPI_LAUNCH((conv3x3_c64_wres<true, true>), grid, dim3(NT), 0, s, a);
   else if (a.res)
-    go(conv3x3_c64_wres<true, false>);
+    SPI_LAUNCH((conv3x3_c64_wres<true, false>), grid, dim3(NT), 0, s, a);
   else if (relu)
-    go(conv3x3_c64_wres<false, true>);
+    SPI_LAUNCH((conv3x3_c64_wres<false, true>), grid, dim3(NT), 0, s, a);
   else
-    go(conv3x3_c64_wres<false, false>);
+    SPI_LAUNCH((conv3x3_c64_wres<false, false>), grid, dim3(NT), 0, s, a);
 }
 
 }  // namespace spi

@@ -418,10 +418,10 @@ void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad, 
                  hipStream_t s) {
   const size_t n = (size_t)B * H * W;
   if (f16)
-    hipLaunchKernelGGL((ingest_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((ingest_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (_Float16*)y, B, C, H, W, cpad);
   else
-    hipLaunchKernelGGL((ingest_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((ingest_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (float*)y, B, C, H, W, cpad);
 }
 
@@ -429,33 +429,33 @@ void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH, in
                   int stride, int pad, bool f16, hipStream_t s) {
   const size_t n = (size_t)B * OH * OW * C / (f16 ? 8 : 4);
   if (f16)
-    hipLaunchKernelGGL((maxpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
+    SPI_LAUNCH((maxpool_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s,
                        (const _Float16*)x, (_Float16*)y, B, H, W, C, OH, OW, k, stride, pad);
   else
-    hipLaunchKernelGGL((maxpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
+    SPI_LAUNCH((maxpool_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s,
                        (const float*)x, (float*)y, B, H, W, C, OH, OW, k, stride, pad);
 }
 
 void maxpool_nhwc_split(const void* x, void* y, int B, int H, int W, int C, int OH, int OW, int k, int stride,
                         int pad, hipStream_t s) {
   const size_t n = (size_t)B * OH * OW * (C / 8);
-  hipLaunchKernelGGL(maxpool_split_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const _Float16*)x, (_Float16*)y, B,
+  SPI_LAUNCH(maxpool_split_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const _Float16*)x, (_Float16*)y, B,
                      H, W, C, OH, OW, k, stride, pad);
 }
 
 void avgpool_nhwc_split(const void* x, float* y, int B, int HW, int C, hipStream_t s) {
-  hipLaunchKernelGGL(avgpool_split_kernel, dim3(B), dim3(256), 0, s, (const _Float16*)x, y, HW, C);
+  SPI_LAUNCH(avgpool_split_kernel, dim3(B), dim3(256), 0, s, (const _Float16*)x, y, HW, C);
 }
 
 void avgpool_nhwc(const void* x, void* y, int B, int HW, int C, bool f16, hipStream_t s, bool out_f32) {
   if (f16 && out_f32)
-    hipLaunchKernelGGL((avgpool_kernel<_Float16, float>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
+    SPI_LAUNCH((avgpool_kernel<_Float16, float>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
                        (float*)y, B, HW, C);
   else if (f16)
-    hipLaunchKernelGGL((avgpool_kernel<_Float16>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
+    SPI_LAUNCH((avgpool_kernel<_Float16>), dim3(B), dim3(256), 0, s, (const _Float16*)x,
                        (_Float16*)y, B, HW, C);
   else
-    hipLaunchKernelGGL((avgpool_kernel<float>), dim3(B), dim3(256), 0, s, (const float*)x,
+    SPI_LAUNCH((avgpool_kernel<float>), dim3(B), dim3(256), 0, s, (const float*)x,
                        (float*)y, B, HW, C);
 }
 
@@ -467,24 +467,24 @@ void layernorm(const float* x, int ldx, const float* g, const float* b, float* y
                    al16(g) && al16(b) && (!yf || al16(yf)) && (!yt || ((reinterpret_cast<uintptr_t>(yt) & 7) == 0));
   if (vec) {
     if (D == 768 && f16)
-      hipLaunchKernelGGL((layernorm_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+      SPI_LAUNCH((layernorm_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
                          (_Float16*)yt, ldy, rows, eps);
     else if (D == 768)
-      hipLaunchKernelGGL((layernorm_vec_kernel<float, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
+      SPI_LAUNCH((layernorm_vec_kernel<float, 3>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
                          ldy, rows, eps);
     else if (f16)
-      hipLaunchKernelGGL((layernorm_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+      SPI_LAUNCH((layernorm_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
                          (_Float16*)yt, ldy, rows, eps);
     else
-      hipLaunchKernelGGL((layernorm_vec_kernel<float, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
+      SPI_LAUNCH((layernorm_vec_kernel<float, 4>), grid, dim3(256), 0, s, x, ldx, g, b, yf, (float*)yt,
                          ldy, rows, eps);
     return;
   }
   if (f16)
-    hipLaunchKernelGGL((layernorm_kernel<_Float16>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+    SPI_LAUNCH((layernorm_kernel<_Float16>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
                        (_Float16*)yt, ldy, rows, D, eps);
   else
-    hipLaunchKernelGGL((layernorm_kernel<float>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
+    SPI_LAUNCH((layernorm_kernel<float>), grid, dim3(256), 0, s, x, ldx, g, b, yf,
                        (float*)yt, ldy, rows, D, eps);
 }
 
@@ -493,32 +493,32 @@ void bert_embed(const int64_t* ids, const float* word, const float* pos, const f
                 int vocab, float eps, bool f16, hipStream_t s) {
   const dim3 grid((B * S + 3) / 4);
   if (f16)
-    hipLaunchKernelGGL((bert_embed_kernel<_Float16>), grid, dim3(256), 0, s, ids, word, pos,
+    SPI_LAUNCH((bert_embed_kernel<_Float16>), grid, dim3(256), 0, s, ids, word, pos,
                        type0, g, b, yf, (_Float16*)yt, B, S, D, vocab, eps);
   else
-    hipLaunchKernelGGL((bert_embed_kernel<float>), grid, dim3(256), 0, s, ids, word, pos,
+    SPI_LAUNCH((bert_embed_kernel<float>), grid, dim3(256), 0, s, ids, word, pos,
                        type0, g, b, yf, (float*)yt, B, S, D, vocab, eps);
 }
 
 void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s) {
-  hipLaunchKernelGGL(mask_bias_kernel, dim3(grid_for(n)), dim3(256), 0, s, mask, bias, n);
+  SPI_LAUNCH(mask_bias_kernel, dim3(grid_for(n)), dim3(256), 0, s, mask, bias, n);
 }
 
 void patchify(const float* x, void* y, int B, int C, int H, int W, int ps, bool f16,
               hipStream_t s) {
   const size_t n = (size_t)B * C * H * W;
   if (f16)
-    hipLaunchKernelGGL((patchify_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((patchify_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (_Float16*)y, B, C, H, W, ps);
   else
-    hipLaunchKernelGGL((patchify_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((patchify_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (float*)y, B, C, H, W, ps);
 }
 
 void vit_assemble(const float* patches, const float* cls, const float* pos, float* x, int B,
                   int P, int D, hipStream_t s) {
   const size_t n = (size_t)B * (P + 1) * D;
-  hipLaunchKernelGGL(vit_assemble_kernel, dim3(grid_for(n)), dim3(256), 0, s, patches, cls,
+  SPI_LAUNCH(vit_assemble_kernel, dim3(grid_for(n)), dim3(256), 0, s, patches, cls,
                      pos, x, B, P, D);
 }
 
@@ -526,15 +526,15 @@ void gather_rows(const float* x, void* y, int rows, int stride_rows, int D, bool
                  hipStream_t s) {
   const size_t n = (size_t)rows * D;
   if (f16)
-    hipLaunchKernelGGL((gather_rows_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((gather_rows_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (_Float16*)y, rows, stride_rows, D);
   else
-    hipLaunchKernelGGL((gather_rows_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
+    SPI_LAUNCH((gather_rows_kernel<float>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (float*)y, rows, stride_rows, D);
 }
 
 void affine(const float* x, float* y, size_t n, float scale, float shift, hipStream_t s) {
-  hipLaunchKernelGGL(affine_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n, scale, shift);
+  SPI_LAUNCH(affine_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n, scale, shift);
 }
 
 }  // namespace spi

@@ -261,6 +261,21 @@ __device__ __forceinline__ void dma_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// One 1-KiB LDS-DMA piece (lane l's 16 bytes from `src` to dst + 16 l) issued from inline
+// asm, invisible to hipcc's waitcnt pass: the epilogue's residual prefetch lands in a stage
+// region addressed at run time, and with the builtin hipcc would assume it may alias the
+// last k-steps' fragment reads and drain it (vmcnt(0)) before them.  Counted by the
+// k-loop's dma_wait_barrier<N> and waited for explicitly before the epilogue reads it.
+__device__ __forceinline__ void glds16(const void* src, char* dst) {
+  const lds_ptr_t lp = (lds_ptr_t)dst;
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lp);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(m0v)
+               : "memory");
+}
+
 template <int RB>
 __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
   constexpr int CPR = RB / 16;  // 16-byte chunks per image row
@@ -663,6 +678,43 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // Residual tile prefetch (64 x 64 tiles on the vector epilogue path): the epilogue's
+  // residual loads were the last dependent memory round trip of a launch (~0.5-1 us of a
+  // ~1.2 us epilogue, tools/gemm_timeline.py).  The tile's residual rows go into LDS by
+  // LDS-DMA at the first k-step that stages no further k-step (step nsteps - STAGES + 1),
+  // into the stage region the step before it used (nsteps % STAGES); the epilogue parks its
+  // fp32 tile in the last step's region ((nsteps - 1) % STAGES), so the two never meet.
+  // Split-K tiles prefetch in the reducing slice only, after its ticket.  res_rb: bytes of a
+  // residual tile row (64 fp16 = 128, 64 fp32 or split = 256); rpw: DMA pieces per wave.
+  constexpr bool RPF = BM == 64 && BN == 64 && !HALO && NW == 4;
+  [[maybe_unused]] const int res_rb = (MODE == kF16X3S || sizeof(typename TR::Out) == 4 || d.res_f32) ? 256 : 128;
+  [[maybe_unused]] const int rpw = res_rb * BM / 1024 / NW;  // 2 or 4
+  [[maybe_unused]] const bool rpf_tile = RPF && a.p.res && a.vec_ok && n0 + BN <= d.N && !d.pool_rows;
+  [[maybe_unused]] const bool rpf_loop = rpf_tile && a.splits == 1;  // prefetched inside the k-loop
+  [[maybe_unused]] const int rpf_step = max(0, nsteps - STAGES + 1);
+  [[maybe_unused]] const int rpf_off = (nsteps % STAGES) * IMG;
+  auto issue_res = [&](char* dst) {
+    if constexpr (RPF) {
+      const int rpp = 1024 / res_rb, cpr = res_rb / 16;  // rows per piece, 16-byte chunks per row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < rpw) {  // wave-uniform
+          const int piece = wave * rpw + q;
+          const int row = piece * rpp + lane / cpr, ch = lane % cpr;
+          const int m = m0 + row;
+          const char* src = zeros;
+          if (m < m_lim) {
+            if constexpr (MODE == kF16X3S)
+              src = reinterpret_cast<const char*>(static_cast<const _Float16*>(a.p.res) + split_idx(m, n0, d.ldr)) + ch * 16;
+            else
+              src = static_cast<const char*>(a.p.res) + ((size_t)m * d.ldr + n0) * (res_rb / 64) + ch * 16;
+          }
+          glds16(src, dst + piece * 1024);
+        }
+      }
+    }
+  };
+
   SPI_RT(rt_p2);
   if constexpr (HALO) issue_halo(h_b0, 0);  // lands before W step 0 (in-order vmcnt)
 #pragma unroll
@@ -679,10 +731,19 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // accesses per thread instead of 128 scalar ones).  All residual loads of a thread
   // go out before its first store (clamped rows: always-valid addresses, no branch).
   // Tiles crossing N, or unaligned strides, take the per-element path from LDS.
-  auto finish = [&](floatx4 (&v)[TI][TJ]) {
+  // toff: byte offset of the parked tile in LDS; rl: the prefetched residual tile (issue_res)
+  // or nullptr (the residual, if any, is read from global memory).
+  auto finish = [&](floatx4 (&v)[TI][TJ], int toff, const char* rl) {
     using Out = typename TR::Out;
     static_assert(BM * BN * 4 <= LDSB - 16, "the C tile must fit the LDS");
-    float* T = reinterpret_cast<float*>(lds);
+    float* T = reinterpret_cast<float*>(lds + toff);
+    // the bias row of this thread's column group, in flight across the park
+    const int nb_ = n0 + (tid % (BN / 8)) * 8;
+    floatx4 bv0 = floatx4{0.f, 0.f, 0.f, 0.f}, bv1 = bv0;
+    if (a.vec_ok && n0 + BN <= d.N && a.p.bias) {
+      bv0 = *reinterpret_cast<const floatx4*>(a.p.bias + nb_);
+      bv1 = *reinterpret_cast<const floatx4*>(a.p.bias + nb_ + 4);
+    }
     __syncthreads();  // every wave is done reading the ring
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -694,6 +755,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           const int col = (wn * WTN + j * 16 + fr) ^ (fq << 4);  // (row >> 2) & 3 == fq
           T[row * BN + col] = v[i][j][r];
         }
+    if (rl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's residual pieces
     __syncthreads();
     if constexpr (!HALO && BM * BN * 4 + 256 * 4 <= LDSB - 16) {
       if (d.pool_rows) {
@@ -776,7 +838,10 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     float b[8];
     if (a.vec_ok && n0 + BN <= d.N) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) b[e] = a.p.bias ? a.p.bias[nb + e] : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        b[e] = bv0[e];
+        b[e + 4] = bv1[e];
+      }
       // rows in chunks of <= 4 per thread: the residual loads of a chunk are all in
       // flight before its first store, within a bounded register budget
       constexpr int CH = ITEMS < 4 ? ITEMS : 4;
@@ -788,7 +853,32 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[it][e] = 0.f;
         }
-        if (a.p.res) {
+        if (RPF && rl) {
+          // the residual tile from LDS ([row][res_rb] as issue_res laid it out)
+#pragma unroll
+          for (int it = 0; it < CH; ++it) {
+            const char* rr = rl + (r0 + (c0 + it) * RSTEP) * res_rb;
+            if constexpr (MODE == kF16X3S) {
+              const char* q = rr + (cg >> 2) * 128 + (cg & 3) * 16;
+              const half8 hi = *reinterpret_cast<const half8*>(q);
+              const half8 lo = *reinterpret_cast<const half8*>(q + 64);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
+            } else if (d.res_f32 || sizeof(Out) == 4) {
+              const floatx4 r0v = *reinterpret_cast<const floatx4*>(rr + cg * 32);
+              const floatx4 r1v = *reinterpret_cast<const floatx4*>(rr + cg * 32 + 16);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                y[it][e] = r0v[e];
+                y[it][e + 4] = r1v[e];
+              }
+            } else {
+              const half8 r = *reinterpret_cast<const half8*>(rr + cg * 16);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(r[e]);
+            }
+          }
+        } else if (a.p.res) {
 #pragma unroll
           for (int it = 0; it < CH; ++it) {
             const int mr = row_m(r0 + (c0 + it) * RSTEP);
@@ -912,20 +1002,34 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         dma_wait_barrier<G * BQ + HQ>();
       else
         dma_wait_barrier<G * BQ>();
-    } else if constexpr (STAGES == 4) {
-      if (t + 2 < nsteps)
-        dma_wait_barrier<2 * QPS>();
-      else if (t + 1 < nsteps)
-        dma_wait_barrier<QPS>();
-      else
-        dma_wait_barrier<0>();
-    } else if constexpr (STAGES == 3) {
-      if (t + 1 < nsteps)
-        dma_wait_barrier<QPS>();
-      else
-        dma_wait_barrier<0>();
     } else {
-      dma_wait_barrier<0>();
+      // steps after the residual prefetch (rpf_loop, issued youngest at rpf_step) also leave
+      // its rpw pieces in flight
+      const bool rx = RPF && rpf_loop && t > rpf_step;
+      auto wait = [&](auto n_c) {
+        constexpr int N = decltype(n_c)::value;
+        if (!rx)
+          dma_wait_barrier<N>();
+        else if (rpw == 2)
+          dma_wait_barrier<N + 2>();
+        else
+          dma_wait_barrier<N + 4>();
+      };
+      if constexpr (STAGES == 4) {
+        if (t + 2 < nsteps)
+          wait(std::integral_constant<int, 2 * QPS>{});
+        else if (t + 1 < nsteps)
+          wait(std::integral_constant<int, QPS>{});
+        else
+          wait(std::integral_constant<int, 0>{});
+      } else if constexpr (STAGES == 3) {
+        if (t + 1 < nsteps)
+          wait(std::integral_constant<int, QPS>{});
+        else
+          wait(std::integral_constant<int, 0>{});
+      } else {
+        wait(std::integral_constant<int, 0>{});
+      }
     }
     SPI_STAMP(st_b);
     // All of this step's fragment reads go out first, then the next step's
@@ -946,6 +1050,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         if (TP == 10 - STAGES && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
       }
       if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
+      if (RPF && rpf_loop && t == rpf_step) issue_res(lds + rpf_off);
     };
     if constexpr (MODE == (int)Prec::F16) {
       half8 af[2][TI], bf[2][TJ];
@@ -1130,45 +1235,59 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   }
 #endif
   if (!kSplitK<BM, BN, KIND> || a.splits == 1) {
-    finish(acc);
+    if (RPF && rpf_loop)
+      finish(acc, ((nsteps - 1) % STAGES) * IMG, lds + rpf_off);
+    else
+      finish(acc, 0, nullptr);
     tl_out(0);
     return;
   }
   if constexpr (kSplitK<BM, BN, KIND>) {
 
-  // ---- split-K: publish this slice's slab, the last arriver reduces -------
-  // Slabs are written in fragment order (thread tid's accumulator (i, j) is 16
-  // contiguous bytes at ((i*TJ + j)*NT + tid)*16), write-through (sc1) so no
-  // release fence is needed; the ticket is a relaxed agent-scope atomic; the
-  // reducer reads every slab with sc1 loads.  Same thread <-> (m, n) map as above.
+  // ---- split-K: the last slice to arrive reduces -----------------------------
+  // Tickets first: a slice that is not last publishes its slab write-through (sc1) in
+  // fragment order (thread tid's accumulator (i, j) is 16 contiguous bytes at
+  // ((i*TJ + j)*NT + tid)*16), drains its stores (vmcnt(0)), and one lane counts the slab
+  // in a second word with a relaxed agent-scope atomic.  The last arriver keeps its own
+  // partial in registers -- no slab store, no read-back -- prefetches the residual,
+  // polls the count (sc1 loads) until every other slab is published, resets both words,
+  // and reads the slabs with sc1 loads (MI355X_MICROARCH.md, the sc1 hand-off).  Every
+  // slice that is not last took its ticket after its k-loop, so the poll ends.  Partials
+  // are summed in split order whichever slice arrives last: deterministic results.
   const int splits = a.splits;
   constexpr int SLAB = BM * BN;
+  int* words = a.p.counters + 2 * tile;  // [0] arrival ticket, [1] published slabs
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(tile_slabs, (short)0, splits * SLAB * 4, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
-    }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (tid == 0) {
-    const int ticket = __hip_atomic_fetch_add(a.p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = ticket == splits - 1;
-    if (last) __hip_atomic_store(a.p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_flag = last;
-  }
+  if (tid == 0) *s_flag = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (!*s_flag) {
+  if (*s_flag < splits - 1) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+      }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (tid == 0) __hip_atomic_fetch_add(words + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tl_out(1);
     return;
   }
-  // ZR splits' slabs in flight per round (two for the small tiles, one when a
-  // slab is 8+ fragments per thread); loads past the last slab fall outside the
-  // descriptor's range and return 0 (no branch, no per-load wait).  Slabs are
-  // summed in split order whichever slice arrives last: deterministic results.
+  const bool rpf_red = RPF && rpf_tile;
+  if (rpf_red) issue_res(lds + IMG);  // the parked tile takes [0, IMG)
+  if (tid == 0) {
+    while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
+      __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_store(words, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(words + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // ZR splits' slabs in flight per round (two for the small tiles, one when a slab is 8+
+  // fragments per thread); loads past the last slab fall outside the descriptor's range and
+  // return 0 (no branch, no per-load wait); this slice's own slot (never written) is
+  // loaded and ignored.
   constexpr int ZR = TI * TJ <= 4 ? 2 : 1;
   floatx4 sum[TI][TJ];
 #pragma unroll
@@ -1187,13 +1306,15 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           v[zz][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
         }
 #pragma unroll
-    for (int zz = 0; zz < ZR; ++zz)
+    for (int zz = 0; zz < ZR; ++zz) {
+      const bool own = z0 + zz == kslice;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) sum[i][j] += v[zz][i][j];
+        for (int j = 0; j < TJ; ++j) sum[i][j] += own ? acc[i][j] : v[zz][i][j];
+    }
   }
-  finish(sum);
+  finish(sum, 0, rpf_red ? lds + IMG : nullptr);
   tl_out(2);
   }
 }
@@ -1471,12 +1592,12 @@ int ilog2(int v) {
 template <int MODE, int BM, int BN, int STAGES, int NW = 4>
 void launch_tile(const KArgs& a, dim3 grid, hipStream_t s) {
   if (a.cell_uniform) {
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvTap, NW>), grid, dim3(64 * NW), 0, s, a);
+    SPI_LAUNCH((gemm_kernel<MODE, BM, BN, STAGES, kConvTap, NW>), grid, dim3(64 * NW), 0, s, a);
   } else if (a.d.conv) {
     if constexpr (MODE != kF16X3S)  // split A needs one tap per step (checked in gemm())
-      hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kConvGen, NW>), grid, dim3(64 * NW), 0, s, a);
+      SPI_LAUNCH((gemm_kernel<MODE, BM, BN, STAGES, kConvGen, NW>), grid, dim3(64 * NW), 0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, STAGES, kDense, NW>), grid, dim3(64 * NW), 0, s, a);
+    SPI_LAUNCH((gemm_kernel<MODE, BM, BN, STAGES, kDense, NW>), grid, dim3(64 * NW), 0, s, a);
   }
 }
 
@@ -1513,7 +1634,7 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   // one (kh, kw) tap per k-step; the per-row tap mask has 32 bits (taps + the Kpad tail step)
   a.cell_uniform = d.conv && d.Cin >= Traits<MODE>::ESTEP && d.KH * d.KW <= 31;
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  a.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res)));
+  a.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res))) && (!p.bias || al16(p.bias));
   if (pl.halo) {
     a.h_th = pl.th;
     a.h_period = pl.period;
@@ -1533,13 +1654,13 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
   if (pl.halo) {
     if constexpr (MODE != (int)Prec::F16X3) {  // fp32 A is split at fragment read: not a halo mode
       if (pl.bm == 256)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, g);
+        SPI_LAUNCH((gemm_kernel<MODE, 256, 64, 3, kConvHalo, 8>), grid, dim3(512), 0, s, g);
       else if (pl.bm == 128)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
+        SPI_LAUNCH((gemm_kernel<MODE, 128, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
       else if (pl.halo == 2)
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, g);
+        SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvHaloS>), grid, dim3(256), 0, s, g);
       else
-        hipLaunchKernelGGL((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
+        SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
     }
     return;
   }
@@ -1562,17 +1683,17 @@ template <int MODE>
 void dispatch_pair(const Plan& pl, const KGroup& g, int wgs, hipStream_t s) {
   const dim3 grid(wgs);
   if (pl.bm == 128 && pl.bn == 128)
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 128, 2, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 128, 128, 2, kConvTap>), grid, dim3(256), 0, s, g);
   else if (pl.bm == 128 && pl.stages == 2)
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 128, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
   else if (pl.bm == 128)
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 128, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 128, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
   else if (pl.stages == 2)
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 64, 64, 2, kConvTap>), grid, dim3(256), 0, s, g);
   else if (pl.stages == 4)
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 4, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 64, 64, 4, kConvTap>), grid, dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL((gemm_kernel_pair<MODE, 64, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
+    SPI_LAUNCH((gemm_kernel_pair<MODE, 64, 64, 3, kConvTap>), grid, dim3(256), 0, s, g);
 }
 
 constexpr Prec prec_of_mode(int mode) { return mode == kF16X3S ? Prec::F16X3 : (Prec)mode; }
@@ -1623,7 +1744,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
   GemmPtrs p1s = p1;
   if (q0.splits > 1) {  // keep clear of problem 0's slabs / tickets
     p1s.partial = p0.partial + (size_t)g.a[0].tiles * q0.splits * q0.bm * q0.bn;
-    p1s.counters = p0.counters + g.a[0].tiles;
+    p1s.counters = p0.counters + 2 * g.a[0].tiles;
   }
   g.a[1] = make_args<MODE>(d1, p1s, q1);
   const bool same = !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
@@ -1649,7 +1770,7 @@ size_t gemm_partial_floats(const GemmDesc& d, Prec prec) {
 size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
   if (pl.splits <= 1) return 0;
-  return (size_t)plan_tiles(d, pl);
+  return 2 * (size_t)plan_tiles(d, pl);  // per tile: arrival ticket + published-slab count
 }
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }

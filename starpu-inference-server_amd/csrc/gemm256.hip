@@ -476,11 +476,11 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
   const dim3 grid(g.tiles_m * g.tiles_n), blk(512);
   if (res == 0)
-    hipLaunchKernelGGL((gemm256_kernel<0>), grid, blk, 0, s, g);
+    SPI_LAUNCH((gemm256_kernel<0>), grid, blk, 0, s, g);
   else if (res == 1)
-    hipLaunchKernelGGL((gemm256_kernel<1>), grid, blk, 0, s, g);
+    SPI_LAUNCH((gemm256_kernel<1>), grid, blk, 0, s, g);
   else
-    hipLaunchKernelGGL((gemm256_kernel<2>), grid, blk, 0, s, g);
+    SPI_LAUNCH((gemm256_kernel<2>), grid, blk, 0, s, g);
 }
 
 }  // namespace spi

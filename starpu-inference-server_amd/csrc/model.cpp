@@ -1159,6 +1159,11 @@ void Model::warmup(hipStream_t s, int B, int S, bool mask) {
 namespace spi {
 
 thread_local std::vector<Model::OpRecord>* Model::prof_ = nullptr;
+
+std::vector<LaunchRec>*& launch_log() {
+  static thread_local std::vector<LaunchRec>* log = nullptr;
+  return log;
+}
 thread_local Model::ProfRepeat* Model::prof_rep_ = nullptr;
 #ifdef SPI_GEMM_TIMELINE
 extern "C" void spi_debug_gemm_timeline_enable(int on, hipStream_t s);
@@ -1177,21 +1182,21 @@ int Model::op_begin(hipStream_t s, const std::string& name, double flops, double
   SPI_HIP(hipEventCreate(&r.stop));
   SPI_HIP(hipEventRecord(r.start, s));
   prof_->push_back(r);
+  launch_log() = &prof_->back().launches;  // until op_end (no other record is pushed meanwhile)
   return r.reps;
 }
 
 void Model::op_end(hipStream_t s) {
+  launch_log() = nullptr;
   SPI_HIP(hipEventRecord(prof_->back().stop, s));
 #ifdef SPI_GEMM_TIMELINE
   if (prof_->back().reps > 1) spi_debug_gemm_timeline_enable(0, s);
 #endif
 }
 
-int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* const* out, float* ms,
-                   double* flops, double* bytes, char* names, int name_len, int max_ops) {
-  if (family_ == SPI_FAMILY_AFFINE) return 0;
+void Model::run_profiled(hipStream_t s, int B, int S, const void* const* in, void* const* out,
+                         std::vector<OpRecord>& recs) {
   if (device_ < 0) throw std::runtime_error("host-only replica (device < 0) cannot run a forward");
-  std::vector<OpRecord> recs;
   Workspace* w = workspace(s);
   prof_ = &recs;
   try {
@@ -1200,10 +1205,23 @@ int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* con
     epilogue(*w, B, S, out, s);
   } catch (...) {
     prof_ = nullptr;
+    launch_log() = nullptr;
+    for (auto& r : recs) {
+      (void)hipEventDestroy(r.start);
+      (void)hipEventDestroy(r.stop);
+    }
+    recs.clear();
     throw;
   }
   prof_ = nullptr;
   SPI_HIP(hipStreamSynchronize(s));
+}
+
+int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* const* out, float* ms,
+                   double* flops, double* bytes, char* names, int name_len, int max_ops) {
+  if (family_ == SPI_FAMILY_AFFINE) return 0;
+  std::vector<OpRecord> recs;
+  run_profiled(s, B, S, in, out, recs);
   int n = 0;
   for (auto& r : recs) {
     if (n < max_ops) {
@@ -1221,14 +1239,26 @@ int Model::profile(hipStream_t s, int B, int S, const void* const* in, void* con
   return n;
 }
 
-}  // namespace spi
+std::string Model::launch_table(hipStream_t s, int B, int S, const void* const* in, void* const* out) {
+  if (family_ == SPI_FAMILY_AFFINE) return "";
+  std::vector<OpRecord> recs;
+  run_profiled(s, B, S, in, out, recs);
+  std::string t;
+  for (size_t i = 0; i < recs.size(); ++i) {
+    for (const LaunchRec& l : recs[i].launches) {
+      // kernel_id's __PRETTY_FUNCTION__: "... [F = &spi::(anonymous namespace)::name<args>]"
+      std::string k = l.kernel;
+      const size_t a = k.find("F = &");
+      if (a != std::string::npos) k = k.substr(a + 5, k.size() - (a + 5) - (k.back() == ']' ? 1 : 0));
+      t += std::to_string(i) + "\t" + recs[i].name + "\t" + k + "\t" + std::to_string(l.gx) + "\t" +
+           std::to_string(l.gy) + "\t" + std::to_string(l.gz) + "\t" + std::to_string(l.block) + "\n";
+    }
+    (void)hipEventDestroy(recs[i].start);
+    (void)hipEventDestroy(recs[i].stop);
+  }
+  return t;
+}
 
-namespace spi {
-
-// One eager forward with op `name` (its first occurrence) launched `reps` times
-// back to back between one pair of events: its steady-state device time per
-// launch, without the event overhead of a single bracketed launch (bench.py's
-// roofline; the same launches a rocprofv3 kernel trace of that command counts).
 int Model::profile_op(hipStream_t s, int B, int S, const void* const* in, void* const* out, const char* name,
                       int reps, float* ms, double* flops, double* bytes) {
   if (!name || reps < 1) throw std::runtime_error("profile_op: name and reps >= 1 required");

@@ -87,9 +87,13 @@ class Model {
     double bytes;
     hipEvent_t start, stop;
     int reps;  // launches between start and stop (profile_op)
+    std::vector<LaunchRec> launches;  // the op's kernel launches (SPI_LAUNCH), in order
   };
   int profile(hipStream_t s, int batch, int S, const void* const* in, void* const* out, float* ms,
               double* flops, double* bytes, char* names, int name_len, int max_ops);
+  // One profiled eager forward as text, one line per kernel launch:
+  // "op_index\top_name\tkernel\tgrid_x\tgrid_y\tgrid_z\tblock\n" (spi_model_launch_table).
+  std::string launch_table(hipStream_t s, int batch, int S, const void* const* in, void* const* out);
   // The same forward with op `name` launched `reps` times back to back; its time per launch.
   int profile_op(hipStream_t s, int batch, int S, const void* const* in, void* const* out, const char* name,
                  int reps, float* ms, double* flops, double* bytes);
@@ -175,6 +179,7 @@ class Model {
 
   std::mutex mu_;
   std::map<hipStream_t, std::unique_ptr<Workspace>> ws_;
+  void run_profiled(hipStream_t s, int B, int S, const void* const* in, void* const* out, std::vector<OpRecord>& recs);
   // Set only inside profile(), on the profiling thread: forwards running on
   // other worker threads at the same time never see it.
   static thread_local std::vector<OpRecord>* prof_;

@@ -5,8 +5,30 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include <cstdint>
+#include <vector>
 
 namespace spi {
+
+// Every kernel launch goes through SPI_LAUNCH.  While a forward is profiled
+// (Model::launch_table) each launch is recorded with its kernel and grid, so a
+// rocprofv3 kernel trace of graph-replayed forwards -- which knows kernels and grids,
+// not ops -- can be attributed to the forward's ops (tools/trace_ops.py --launches).
+// Outside profiling the cost is one thread-local pointer test per launch.
+struct LaunchRec {
+  const char* kernel;  // __PRETTY_FUNCTION__ of kernel_id<F>: "... [F = &spi::...::name<args>]"
+  unsigned gx, gy, gz, block;
+};
+std::vector<LaunchRec>*& launch_log();
+template <auto F>
+inline const char* kernel_id() {
+  return __PRETTY_FUNCTION__;
+}
+#define SPI_LAUNCH(F, G, B, SH, S, ...)                                                                  \
+  do {                                                                                                   \
+    if (auto* spi_log_ = ::spi::launch_log())                                                            \
+      spi_log_->push_back({::spi::kernel_id<F>(), dim3(G).x, dim3(G).y, dim3(G).z, dim3(B).x});          \
+    hipLaunchKernelGGL(F, G, B, SH, S, __VA_ARGS__);                                                     \
+  } while (0)
 
 enum class Act : int { None = 0, Relu = 1, Gelu = 2 };
 

@@ -304,11 +304,11 @@ void launch_pr(const float* x, const _Float16* w, const float* bias, void* y, in
 #endif
   const dim3 grid((PH + PR - 1) / PR, B), block(64 * NW);
   if (split)
-    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, true, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, true, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
   else if (lo)
-    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, true, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, true, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
   else
-    hipLaunchKernelGGL((stem_pool_kernel<PR, NW, false, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, false, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
 }
 
 }  // namespace
