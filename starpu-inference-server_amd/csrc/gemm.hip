@@ -27,6 +27,7 @@
 // them with sc1 loads and runs the epilogue -- no second launch, no cache-wide
 // fences (cdna_hip_programming.md, "In-launch split-K reduction").
 #include "device_math.hpp"
+#include "ln_fold.hpp"
 #include "spi_kernels.hpp"
 
 #include <algorithm>
@@ -66,7 +67,12 @@ __device__ unsigned long long g_gemm_stamps[65536 * 8];
 // onto CUs.  The real kernel has none of this.
 #ifdef SPI_GEMM_TIMELINE
 __device__ unsigned long long g_gemm_timeline[65536 * 8];
-__device__ int g_gemm_timeline_on;
+// launches made by a thread inside spi_debug_gemm_timeline_enable(1) .. (0) carry KArgs::tl = 1
+// (Model::profile_op on the repeated op), so other streams' launches never stamp
+int& tl_thread() {
+  static thread_local int on = 0;
+  return on;
+}
 #define SPI_RT(v)                                                                  \
   do {                                                                             \
     __builtin_amdgcn_sched_barrier(0);                                             \
@@ -172,6 +178,9 @@ struct KArgs {
   // blocks, h_bps of them per split-K slice
   int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
   int splits;  // split-K slices (the grid holds tiles x splits workgroups of this problem)
+#ifdef SPI_GEMM_TIMELINE
+  int tl;  // stamp this launch (tools/gemm_timeline.py)
+#endif
 };
 
 // One launch, one or two independent problems of the same kernel instance (a
@@ -358,7 +367,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   auto tl_out = [&](int kind) {
     unsigned long long rt_x;
     SPI_RT(rt_x);
-    if (threadIdx.x == 0 && g_gemm_timeline_on) {
+    if (threadIdx.x == 0 && a.tl) {
       unsigned long long* g = g_gemm_timeline + (size_t)((blockIdx.x + blockIdx.y * gridDim.x) & 65535) * 8;
       g[0] = rt_e;
       g[1] = rt_l0;
@@ -687,6 +696,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // Split-K tiles prefetch in the reducing slice only, after its ticket.  res_rb: bytes of a
   // residual tile row (64 fp16 = 128, 64 fp32 or split = 256); rpw: DMA pieces per wave.
   constexpr bool RPF = BM == 64 && BN == 64 && !HALO && NW == 4;
+  // the LayerNorm fold lives in the dense fp16 instances only (the transformer GEMMs)
+  constexpr bool LNF = KIND == kDense && MODE == (int)Prec::F16;
   [[maybe_unused]] const int res_rb = (MODE == kF16X3S || sizeof(typename TR::Out) == 4 || d.res_f32) ? 256 : 128;
   [[maybe_unused]] const int rpw = res_rb * BM / 1024 / NW;  // 2 or 4
   [[maybe_unused]] const bool rpf_tile = RPF && a.p.res && a.vec_ok && n0 + BN <= d.N && !d.pool_rows;
@@ -842,6 +853,25 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         b[e] = bv0[e];
         b[e + 4] = bv1[e];
       }
+      // LayerNorm fold vectors of this thread's 8 columns: c1 (consumer), gain / bias of the
+      // residual's LayerNorm (res_ln)
+      [[maybe_unused]] float lnc1[8], lng[8], lnb[8];
+      if constexpr (LNF) {
+        const auto ld8 = [&](const float* v, float (&o)[8]) {
+          const floatx4 x0 = *reinterpret_cast<const floatx4*>(v + nb);
+          const floatx4 x1 = *reinterpret_cast<const floatx4*>(v + nb + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = x0[e];
+            o[e + 4] = x1[e];
+          }
+        };
+        if (d.ln_in_chunks > 0) ld8(a.p.ln.c1, lnc1);
+        if (d.res_ln_chunks > 0) {
+          ld8(a.p.ln.res_g, lng);
+          ld8(a.p.ln.res_b, lnb);
+        }
+      }
       // rows in chunks of <= 4 per thread: the residual loads of a chunk are all in
       // flight before its first store, within a bounded register budget
       constexpr int CH = ITEMS < 4 ? ITEMS : 4;
@@ -906,14 +936,53 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
             }
           }
         }
+        if constexpr (LNF) {
+          // LayerNorm fold (ln_fold.hpp): the residual as LN(R) of the fp32 rows R loaded above
+          if (d.res_ln_chunks > 0) {
+#pragma unroll
+            for (int it = 0; it < CH; ++it) {
+              const int mr = row_m(r0 + (c0 + it) * RSTEP);
+              float mean, rstd;
+              ln_row_stats(a.p.ln.res_stats, mr < 0 ? 0 : mr, d.res_ln_chunks, d.res_ln_eps, mean, rstd);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = (y[it][e] - mean) * rstd * lng[e] + lnb[e];
+            }
+          }
+        }
 #pragma unroll
         for (int it = 0; it < CH; ++it) {
           float t[8];
           tile_vals(r0 + (c0 + it) * RSTEP, t);
+          if constexpr (LNF) {
+            if (d.ln_in_chunks > 0) {  // consumer: y = rstd (acc - mean c1) + bias
+              const int mr = row_m(r0 + (c0 + it) * RSTEP);
+              float mean, rstd;
+              ln_row_stats(a.p.ln.in_stats, mr < 0 ? 0 : mr, d.ln_in_chunks, d.ln_in_eps, mean, rstd);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) t[e] = rstd * (t[e] - mean * lnc1[e]);
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[it][e] = t[e] + b[e] + y[it][e];  // acc + bias + residual
         }
         finish_act(y);
+        if constexpr (LNF) {
+          if (d.ln_out) {  // producer: chunk statistics + the fp16 copy of every output row
+#pragma unroll
+            for (int it = 0; it < CH; ++it) {
+              const int m = row_m(r0 + (c0 + it) * RSTEP);
+              float mean, m2;
+              ln_chunk_stats(y[it], mean, m2);  // lanes of one row: consecutive cg
+              if (m < 0) continue;
+              if ((cg & 7) == 0)
+                reinterpret_cast<float2*>(a.p.ln.out_stats)[(size_t)m * (d.N >> 6) + (nb >> 6)] = float2{mean, m2};
+              half8 h;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(y[it][e]);
+              *reinterpret_cast<half8*>(a.p.ln.c16 + (size_t)m * d.ld16 + nb) = h;
+            }
+          }
+        }
 #pragma unroll
         for (int it = 0; it < CH; ++it) {
           const int m = row_m(r0 + (c0 + it) * RSTEP);
@@ -1611,6 +1680,9 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   a.splits = pl.splits;
   a.tiles = plan_tiles(d, pl);
   a.tiles_m = a.tiles / ((d.N + pl.bn - 1) / pl.bn);
+#ifdef SPI_GEMM_TIMELINE
+  a.tl = tl_thread();
+#endif
   const int TM = a.tiles_m, TN = a.tiles / a.tiles_m;
   a.tiles_n = TN;
   xcd_groups(d, MODE == kF16X3S ? Prec::F16X3 : (Prec)MODE, TM, TN, a.xg_m, a.xg_n);
@@ -1791,11 +1863,7 @@ extern "C" int spi_debug_gemm_stamps(unsigned long long* host, size_t n) {
 extern "C" int spi_debug_gemm_timeline(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_timeline), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
-extern "C" void spi_debug_gemm_timeline_enable(int on, hipStream_t s) {
-  static const int vals[2] = {0, 1};  // stream-ordered: the source must outlive the copy
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gemm_timeline_on), &vals[on ? 1 : 0], sizeof(int), 0,
-                               hipMemcpyHostToDevice, s);
-}
+extern "C" void spi_debug_gemm_timeline_enable(int on, hipStream_t) { tl_thread() = on; }
 extern "C" int spi_debug_gemm_timeline_clear(void) {
   static unsigned long long zeros[65536 * 8];
   return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_timeline), zeros, sizeof(zeros)) == hipSuccess ? 0 : 1;
@@ -1841,6 +1909,18 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 
 void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
   check_desc(d, prec);
+  if (d.ln_in_chunks > 0 || d.res_ln_chunks > 0 || d.ln_out) {
+    // the fold lives in the dense fp16 kernels' vector epilogue: whole 128-column tiles,
+    // 16-byte aligned rows everywhere it reads or writes
+    const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const bool ok = prec == Prec::F16 && !d.conv && !d.pool_rows && d.krep == 1 && d.N % 128 == 0 &&
+                    d.ldc % 8 == 0 && al16(p.C) && (!p.bias || al16(p.bias)) &&
+                    (!p.res || (d.ldr % 8 == 0 && al16(p.res))) &&
+                    (d.ln_in_chunks == 0 || (p.ln.in_stats && p.ln.c1 && al16(p.ln.c1))) &&
+                    (d.res_ln_chunks == 0 || (p.res && d.res_f32 && p.ln.res_stats && al16(p.ln.res_g) && al16(p.ln.res_b))) &&
+                    (!d.ln_out || (p.ln.out_stats && p.ln.c16 && al16(p.ln.c16) && d.ld16 % 8 == 0));
+    if (!ok) throw std::invalid_argument("LayerNorm fold: dense fp16 GEMM, N % 128 == 0, aligned vectors");
+  }
   switch (prec) {
     case Prec::F16:
       if (conv_wres_eligible(d, prec, p))

@@ -26,6 +26,7 @@
 // rows, 16-byte chunk c of row r at slot c ^ (r & 7), swizzle applied on the
 // DMA source address (rule 21), conflict-free ds_read_b128 fragment reads.
 #include "device_math.hpp"
+#include "ln_fold.hpp"
 #include "spi_kernels.hpp"
 
 #include <cstdlib>
@@ -51,6 +52,14 @@ struct G256Args {
   int act;  // Act
   int res_f32, out_f32;
   int vec_ok;  // C / residual rows and pointers allow 16-byte vectors (LDS-staged epilogue)
+  // LayerNorm fold (GemmDesc::ln_in_chunks / ln_out, ln_fold.hpp): consumer statistics of the
+  // A rows + c1; producer statistics + fp16 copy of the output
+  int ln_in_chunks, ln_out, ld16;
+  float ln_in_eps;
+  const float* ln_in_stats;
+  const float* ln_c1;
+  float* ln_out_stats;
+  _Float16* c16;
 };
 
 constexpr int kBufBytes = 65536;  // one k-tile: A 256 x 128 B + B 256 x 128 B
@@ -294,7 +303,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   float* T = reinterpret_cast<float*>(lds);
   const int cg = tid & 31, r0 = tid >> 5;  // 8-column group, first row of this thread
   const int nb = n0 + 8 * cg;
-  float bias8[8];
+  float bias8[8], c18[8];
+  if (g.ln_in_chunks > 0) {
+    const floatx4 c0 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb);
+    const floatx4 c1 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      c18[e] = c0[e];
+      c18[e + 4] = c1[e];
+    }
+  }
   if (g.bias) {
     const floatx4 b0 = *reinterpret_cast<const floatx4*>(g.bias + nb);
     const floatx4 b1 = *reinterpret_cast<const floatx4*>(g.bias + nb + 4);
@@ -384,8 +402,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           }
           float y[8];
 #pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = e < 4 ? x0[e] : x1[e - 4];
+          if (g.ln_in_chunks > 0) {  // LayerNorm of the A rows folded in: rstd (acc - mean c1)
+            float mean, rstd;
+            ln_row_stats(g.ln_in_stats, min(m, g.M - 1), g.ln_in_chunks, g.ln_in_eps, mean, rstd);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = rstd * (y[e] - mean * c18[e]);
+          }
+#pragma unroll
           for (int e = 0; e < 8; ++e) {
-            y[e] = (e < 4 ? x0[e] : x1[e - 4]) + bias8[e] + r[e];
+            y[e] += bias8[e] + r[e];
             if constexpr (ACT == (int)Act::Relu) y[e] = y[e] > 0.f ? y[e] : 0.f;
           }
           if constexpr (ACT == (int)Act::Gelu) {
@@ -401,6 +427,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           // could, races with the real row M - 1 when C is the residual buffer itself -- the
           // transformer's in-place residual stream: a duplicate that reads the residual after the
           // real row's store adds the GEMM twice.)
+          if (g.ln_out) {  // producer: chunk statistics (all lanes shuffle) + the fp16 copy
+            float mean, m2;
+            ln_chunk_stats(y, mean, m2);
+            if (m < g.M) {
+              if ((cg & 7) == 0)
+                reinterpret_cast<float2*>(g.ln_out_stats)[(size_t)m * (g.N >> 6) + (nb >> 6)] = float2{mean, m2};
+              half8 hq;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) hq[e] = static_cast<_Float16>(y[e]);
+              *reinterpret_cast<half8*>(g.c16 + (size_t)m * g.ld16 + nb) = hq;
+            }
+          }
           if constexpr (GUARD) {
             if (m >= g.M) continue;
           }
@@ -473,6 +511,17 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   g.vec_ok = d.ldc % 8 == 0 && al16(p.C) && (!p.res || (d.ldr % 8 == 0 && al16(p.res))) && (!p.bias || al16(p.bias))
                  ? 1 : 0;
+  g.ln_in_chunks = d.ln_in_chunks;
+  g.ln_in_eps = d.ln_in_eps;
+  g.ln_out = d.ln_out ? 1 : 0;
+  g.ld16 = d.ld16;
+  g.ln_in_stats = p.ln.in_stats;
+  g.ln_c1 = p.ln.c1;
+  g.ln_out_stats = p.ln.out_stats;
+  g.c16 = p.ln.c16;
+  if ((d.ln_in_chunks > 0 || d.ln_out) && !g.vec_ok)
+    throw std::invalid_argument("gemm256: the LayerNorm fold needs the vector epilogue");
+  if (d.res_ln_chunks > 0) throw std::invalid_argument("gemm256: no residual LayerNorm (post-LN) epilogue");
   const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
   const dim3 grid(g.tiles_m * g.tiles_n), blk(512);
   if (res == 0)

@@ -245,6 +245,37 @@ LinearW pack_linear_named(const PMap& p, const std::string& name, Prec prec, boo
   return pack_linear(fdata(wt), b, (int)wt->shape[0], (int)wt->shape[1], prec, hilo);
 }
 
+// The weights of a GEMM whose input rows are LayerNorm'd (y = LN(x) W^T + b), packed for
+// the fold (ln_fold.hpp): W' = W diag(gamma) in the compute type, bias' = b + W beta, and
+// c1[n] = sum_k W'[n][k] over the packed (rounded) values, so the epilogue's
+// rstd (x W'^T - mean c1) cancels exactly what the MFMAs accumulated.
+LinearW pack_linear_folded(const float* w, const float* b, int N, int K, Prec prec, const float* gamma,
+                           const float* beta) {
+  std::vector<float> wf((size_t)N * K), bf(N);
+  std::vector<float> c1(N);
+  for (int n = 0; n < N; ++n) {
+    double bb = b ? b[n] : 0.0, cc = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const float v = w[(size_t)n * K + k];
+      const float f = v * gamma[k];
+      wf[(size_t)n * K + k] = f;
+      bb += (double)beta[k] * v;
+      cc += prec == Prec::F16 ? (double)static_cast<float>(static_cast<_Float16>(f)) : (double)f;
+    }
+    bf[n] = (float)bb;
+    c1[n] = (float)cc;
+  }
+  LinearW L = pack_linear(wf.data(), bf.data(), N, K, prec);
+  L.c1 = pack_vec(c1.data(), N);
+  return L;
+}
+
+// SPI_LN_FOLD=0: the separate LayerNorm launches (A/B runs); the fold is an fp16 path
+bool ln_fold_enabled(Prec prec) {
+  const char* e = std::getenv("SPI_LN_FOLD");
+  return prec == Prec::F16 && !(e && *e && std::atoi(e) == 0);
+}
+
 LnW pack_ln(const PMap& p, const std::string& name) {
   LnW l;
   const spi_named_tensor* g = need(p, name + ".weight");
@@ -329,12 +360,14 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     os << "] img" << image_ << " classes" << classes_;
   } else if (family_ == SPI_FAMILY_BERT) {
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-12f;
+    ln_fold_ = ln_fold_enabled(prec_);
     heads_ = cfg.num_heads;
     seq_ = cfg.seq_len;
     build_bert(strip_prefix(p, "embeddings.word_embeddings.weight"));
     os << "bert L" << layers_ << " D" << D_ << " H" << heads_ << " FF" << ffn_ << " S<=" << seq_;
   } else if (family_ == SPI_FAMILY_VIT) {
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-6f;
+    ln_fold_ = ln_fold_enabled(prec_);
     heads_ = cfg.num_heads;
     if (cfg.image_size > 0) image_ = cfg.image_size;
     build_vit(strip_prefix(p, "conv_proj.weight"));
@@ -497,6 +530,28 @@ void Model::build_bert(const PMap& p) {
     ffn_ = L.ff1.n;
     tf_.push_back(L);
   }
+  // post-LN: FFN1 of layer i reads LN1_i(a), QKV of layer i >= 1 reads LN2_{i-1}(b)
+  ln_fold_ = ln_fold_ && D_ % 128 == 0 && ffn_ % 128 == 0;
+  if (ln_fold_) {
+    for (int i = 0; i < layers_; ++i) {
+      const std::string pre = "encoder.layer." + std::to_string(i) + ".";
+      const std::string ln1 = pre + "attention.output.LayerNorm";
+      const spi_named_tensor* f1 = need(p, pre + "intermediate.dense.weight");
+      tf_[i].ff1 = pack_linear_folded(fdata(f1), fdata(need(p, pre + "intermediate.dense.bias")), ffn_, D_, prec_,
+                                      fdata(need(p, ln1 + ".weight")), fdata(need(p, ln1 + ".bias")));
+      if (i == 0) continue;
+      const std::string ln2 = "encoder.layer." + std::to_string(i - 1) + ".output.LayerNorm";
+      std::vector<float> w((size_t)3 * D_ * D_), b((size_t)3 * D_);
+      const char* names[3] = {"query", "key", "value"};
+      for (int j = 0; j < 3; ++j) {
+        const std::string nm = pre + "attention.self." + names[j];
+        std::memcpy(w.data() + (size_t)j * D_ * D_, fdata(need(p, nm + ".weight")), sizeof(float) * D_ * D_);
+        std::memcpy(b.data() + (size_t)j * D_, fdata(need(p, nm + ".bias")), sizeof(float) * D_);
+      }
+      tf_[i].qkv = pack_linear_folded(w.data(), b.data(), 3 * D_, D_, prec_, fdata(need(p, ln2 + ".weight")),
+                                      fdata(need(p, ln2 + ".bias")));
+    }
+  }
 }
 
 void Model::build_vit(const PMap& p) {
@@ -533,6 +588,23 @@ void Model::build_vit(const PMap& p) {
     L.ff2 = pack_linear_named(p, m2, prec_);
     ffn_ = L.ff1.n;
     tf_.push_back(L);
+  }
+  // pre-LN: QKV of layer i >= 1 reads LN1_i(x) (layer 0's LN1 stays a launch: the stream
+  // comes from vit_assemble), FFN1 of layer i reads LN2_i(x)
+  ln_fold_ = ln_fold_ && D_ % 128 == 0 && ffn_ % 128 == 0;
+  if (ln_fold_) {
+    for (int i = 0; i < layers_; ++i) {
+      const std::string pre = "encoder.layers.encoder_layer_" + std::to_string(i) + ".";
+      const std::string m1 = has(p, pre + "mlp.0.weight") ? pre + "mlp.0" : pre + "mlp.linear_1";
+      const spi_named_tensor* f1 = need(p, m1 + ".weight");
+      tf_[i].ff1 = pack_linear_folded(fdata(f1), fdata(need(p, m1 + ".bias")), (int)f1->shape[0], (int)f1->shape[1],
+                                      prec_, fdata(need(p, pre + "ln_2.weight")), fdata(need(p, pre + "ln_2.bias")));
+      if (i == 0) continue;
+      const spi_named_tensor* iw = need(p, pre + "self_attention.in_proj_weight");
+      tf_[i].qkv = pack_linear_folded(fdata(iw), fdata(need(p, pre + "self_attention.in_proj_bias")),
+                                      (int)iw->shape[0], (int)iw->shape[1], prec_, fdata(need(p, pre + "ln_1.weight")),
+                                      fdata(need(p, pre + "ln_1.bias")));
+    }
   }
   final_ln_ = pack_ln(p, "encoder.ln");
   head_ = pack_linear_named(p, "heads.head", prec_);
@@ -752,13 +824,36 @@ void Model::run_conv_pair(const ConvW& c0, const void* x, int B, int H, int W, v
 }
 
 void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc, bool out_f32, Act act,
-                     const void* res, bool res_f32, int ldr, Workspace& ws, hipStream_t s) {
+                     const void* res, bool res_f32, int ldr, Workspace& ws, hipStream_t s, const LnSpec* ln) {
   GemmDesc d = linear_desc(L, M, lda, ldc);
   d.act = act;
   d.out_f32 = out_f32;
   d.res_f32 = res_f32;
   d.ldr = ldr;
   d.wplane = L.wplane;
+  LnPtrs lp;
+  if (ln) {
+    if (ln->in_stats) {
+      if (!L.c1) throw std::runtime_error("LayerNorm fold: the GEMM's weights were not packed folded");
+      d.ln_in_chunks = L.k / 64;
+      d.ln_in_eps = eps_;
+      lp.in_stats = ln->in_stats;
+      lp.c1 = ptr<float>(L.c1);
+    }
+    if (ln->res_stats) {
+      d.res_ln_chunks = L.n / 64;
+      d.res_ln_eps = eps_;
+      lp.res_stats = ln->res_stats;
+      lp.res_g = ln->res_g;
+      lp.res_b = ln->res_b;
+    }
+    if (ln->out_stats) {
+      d.ln_out = true;
+      d.ld16 = L.n;
+      lp.out_stats = ln->out_stats;
+      lp.c16 = static_cast<_Float16*>(ln->c16);
+    }
+  }
   const size_t es = f16_ ? 2 : 4;
   const int nrep = !prof_ ? 1 : op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
              2.0 * M * L.n * (double)L.k,
@@ -773,6 +868,7 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   p.partial = ws.partial;
   p.counters = ws.counters;
   p.zeros = dblob_;  // the blob starts with a zeroed 256-byte line
+  p.ln = lp;
   if (gemm_partial_floats(d, L.prec) > ws.partial_floats || gemm_counter_slots(d, L.prec) > kCounterSlots)
     throw std::runtime_error("split-K workspace too small");
   for (int r = 0; r < nrep; ++r) gemm(d, p, L.prec, s);
@@ -862,7 +958,8 @@ Workspace* Model::workspace(hipStream_t s) {
     sizes.push_back((size_t)B * feat_ * ea);  // pooled (fp32 under F16M: the FC's A)
   } else if (family_ == SPI_FAMILY_BERT) {
     const size_t T = (size_t)B * seq_;
-    sizes = {T * D_ * 4, T * D_ * es, T * 3 * D_ * es, T * D_ * es, T * D_ * 4, T * ffn_ * es};
+    sizes = {T * D_ * 4, T * D_ * es, T * 3 * D_ * es, T * D_ * es, T * D_ * 4, T * ffn_ * es,
+             T * (D_ / 64) * 8, T * (D_ / 64) * 8};  // 6, 7: LayerNorm-fold row statistics S1, S2
     for (const auto& L : tf_)
       partial = std::max({partial, linear_partial(L.qkv, (int)T), linear_partial(L.out, (int)T),
                           linear_partial(L.ff1, (int)T), linear_partial(L.ff2, (int)T)});
@@ -876,7 +973,8 @@ Workspace* Model::workspace(hipStream_t s) {
              T * 3 * D_ * es,                           // 4 qkv
              T * D_ * es,                               // 5 ctx
              T * ffn_ * es,                             // 6 mlp hidden
-             (size_t)B * D_ * es};                      // 7 cls
+             (size_t)B * D_ * es,                       // 7 cls
+             T * (D_ / 64) * 8};                        // 8 LayerNorm-fold row statistics of x
     partial = std::max(partial, linear_partial(patch_proj_, B * npatch_));
     for (const auto& L : tf_)
       partial = std::max({partial, linear_partial(L.qkv, (int)T), linear_partial(L.out, (int)T),
@@ -1022,6 +1120,49 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     float* a = static_cast<float*>(w.bufs[4]);
     void* ff = w.bufs[5];
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
+    if (ln_fold_) {
+      // Post-LN with the LayerNorms folded (ln_fold.hpp): hf holds the embedding output, then
+      // each layer's pre-LN2 rows b; a the pre-LN1 rows; ht the fp16 copy the next GEMM reads;
+      // S1 / S2 their row statistics.  Layer i:
+      //   qkv  = LN2_{i-1}(b) Wqkv  (folded; layer 0 reads the embedding output)
+      //   a    = ctx Wo + LN2_{i-1}(b)    -> S1, ht
+      //   ff   = GELU(LN1_i(a) W1)  (folded)
+      //   b    = ff W2 + LN1_i(a)         -> S2, ht
+      // and the epilogue runs the one LayerNorm left, LN2 of the last layer.
+      float* S1 = static_cast<float*>(w.bufs[6]);
+      float* S2 = static_cast<float*>(w.bufs[7]);
+      for (int i = 0; i < layers_; ++i) {
+        const TfLayer& L = tf_[i];
+        LnSpec q;
+        if (i > 0) q.in_stats = S2;
+        run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
+        const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
+                                               (double)T * 4 * D_ * 2);
+        for (int r = 0; r < nrep; ++r)
+          attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
+        if (prof_) op_end(s);
+        LnSpec o;
+        if (i > 0) {
+          o.res_stats = S2;
+          o.res_g = ptr<float>(tf_[i - 1].ln2.g);
+          o.res_b = ptr<float>(tf_[i - 1].ln2.b);
+        }
+        o.out_stats = S1;
+        o.c16 = ht;
+        run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s, &o);
+        LnSpec f1;
+        f1.in_stats = S1;
+        run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
+        LnSpec f2;
+        f2.res_stats = S1;
+        f2.res_g = ptr<float>(L.ln1.g);
+        f2.res_b = ptr<float>(L.ln1.b);
+        f2.out_stats = S2;
+        f2.c16 = ht;
+        run_gemm(L.ff2, ff, T, ffn_, hf, D_, true, Act::None, a, true, D_, w, s, &f2);
+      }
+      return;
+    }
     for (int i = 0; i < layers_; ++i) {
       const TfLayer& L = tf_[i];
       run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s);
@@ -1052,6 +1193,37 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
     });
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
+    if (ln_fold_) {
+      // Pre-LN with the LayerNorms folded (ln_fold.hpp): the GEMMs that update the residual
+      // stream x (in place) write its row statistics Sx and an fp16 copy (buf 3); the QKV
+      // (layer >= 1) and FFN1 GEMMs read that copy with LN1 / LN2 folded in.  Only layer 0's
+      // LN1 runs as a launch (x comes from vit_assemble).
+      float* Sx = static_cast<float*>(buf[8]);
+      for (int i = 0; i < layers_; ++i) {
+        const TfLayer& L = tf_[i];
+        LnSpec q;
+        if (i == 0) {
+          prof_op(s, "layernorm", ln_bytes(T, false), [&] {
+            layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), nullptr, buf[3], D_, T, D_, eps_, f16_, s);
+          });
+        } else {
+          q.in_stats = Sx;
+        }
+        run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
+        const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
+                                               (double)T * 4 * D_ * 2);
+        for (int r = 0; r < nrep; ++r) attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
+        if (prof_) op_end(s);
+        LnSpec o;
+        o.out_stats = Sx;
+        o.c16 = buf[3];
+        run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s, &o);
+        LnSpec f1;
+        f1.in_stats = Sx;
+        run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
+        run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w, s, &o);
+      }
+    } else {
     for (const TfLayer& L : tf_) {
       prof_op(s, "layernorm", ln_bytes(T, false), [&] {
         layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
@@ -1069,6 +1241,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       });
       run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s);
       run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w, s);
+    }
     }
     // final LN on the class-token rows only (torchvision: x = ln(x); x = x[:, 0])
     prof_op(s, "layernorm_cls", ln_bytes(B, false), [&] {
@@ -1088,7 +1261,8 @@ void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s
     const TfLayer& L = tf_.back();
     const int T = B * S;
     prof_op(s, "layernorm_out", (double)T * D_ * 8, [&] {
-      layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
+      // the last layer's pre-LN2 rows: hf under the LayerNorm fold, else a
+      layernorm(static_cast<float*>(w.bufs[ln_fold_ ? 0 : 4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
                 static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
     });
   } else if (family_ == SPI_FAMILY_VIT) {

@@ -31,6 +31,7 @@ struct ConvW {
 
 struct LinearW {
   size_t w = 0, b = 0;
+  size_t c1 = 0;  // LayerNorm fold (GemmDesc::ln_in_chunks): sum_k W'[n][k] of the folded weights, else 0
   int n = 0, k = 0, kpad = 0, npad = 0;
   size_t wplane = 0;
   bool has_bias = true;
@@ -112,9 +113,18 @@ class Model {
   void body(Workspace& w, int batch, int S, hipStream_t s);
   void prologue(Workspace& w, int batch, int S, const void* const* in, hipStream_t s);
   void epilogue(Workspace& w, int batch, int S, void* const* out, hipStream_t s);
+  // The LayerNorm fold of one transformer GEMM (ln_fold.hpp).
+  struct LnSpec {
+    const float* in_stats = nullptr;  // A rows are pre-LN: their chunk statistics (L.c1 folded in)
+    const float* res_stats = nullptr;  // residual is LN(R): R's statistics, gain, bias
+    const float* res_g = nullptr;
+    const float* res_b = nullptr;
+    float* out_stats = nullptr;  // write the output's statistics ...
+    void* c16 = nullptr;         // ... and an fp16 copy
+  };
   void run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc,
                 bool out_f32, Act act, const void* res, bool res_f32, int ldr, Workspace& ws,
-                hipStream_t s);
+                hipStream_t s, const LnSpec* ln = nullptr);
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
                 Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32 = false,
                 bool res_f32 = false);
@@ -169,6 +179,9 @@ class Model {
   // transformers
   int D_ = 768, heads_ = 12, ffn_ = 3072, seq_ = 128, layers_ = 0, vocab_ = 0, maxpos_ = 0;
   float eps_ = 1e-12f;
+  // LayerNorm folded across the GEMMs (fp16, D and FFN multiples of 128; SPI_LN_FOLD=0: the
+  // separate LayerNorm launches): no LN launch inside the encoder stack
+  bool ln_fold_ = false;
   size_t word_ = 0, pos_ = 0, type0_ = 0;
   LnW emb_ln_, final_ln_;
   std::vector<TfLayer> tf_;

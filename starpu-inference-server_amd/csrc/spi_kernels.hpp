@@ -77,6 +77,33 @@ struct GemmDesc {
   // W came from pack_matrix_into of an fp16 64 x 576 matrix, whose padding rows 64..127
   // hold the weight-resident conv's LDS image (pack.hpp); conv_wres requires it.
   bool w_image = false;
+  // LayerNorm folded across GEMMs (transformer fp16 path; dense F16 A, the
+  // vector epilogue only).  Row statistics travel as per-64-column-chunk partials
+  // (mean, M2) -- [rows][chunks][2] fp32 -- combined by Chan's formula where they are used.
+  //  ln_in_chunks > 0: A holds the rows x BEFORE a LayerNorm (an fp16 copy), W was packed
+  //    with the gain folded in (W' = W diag(gamma)), and the epilogue applies
+  //    y = rstd[m] * (acc - mean[m] * c1[n]) + bias[n] (bias = b + W beta, c1 = W' 1).
+  //  res_ln_chunks > 0: the residual is LN(R) computed on the fly from the fp32 rows R and
+  //    their statistics: (R - mean) * rstd * g + b (a post-LN block's input).
+  //  ln_out: write the output rows' chunk statistics (N / 64 chunks) and an fp16 copy of
+  //    the output (C16, row stride ld16) for the next, folding GEMM.
+  int ln_in_chunks = 0;
+  float ln_in_eps = 0.f;
+  int res_ln_chunks = 0;
+  float res_ln_eps = 0.f;
+  bool ln_out = false;
+  int ld16 = 0;
+};
+
+// Pointers of the LayerNorm fold (GemmDesc::ln_in_chunks / res_ln_chunks / ln_out).
+struct LnPtrs {
+  const float* in_stats = nullptr;   // A rows' chunk statistics
+  const float* c1 = nullptr;         // [N] per-column sum of the folded weights
+  const float* res_stats = nullptr;  // residual rows' chunk statistics
+  const float* res_g = nullptr;      // residual LayerNorm gain / bias
+  const float* res_b = nullptr;
+  float* out_stats = nullptr;        // output rows' chunk statistics
+  _Float16* c16 = nullptr;           // fp16 copy of the output
 };
 
 struct GemmPtrs {
@@ -88,6 +115,7 @@ struct GemmPtrs {
   float* partial = nullptr;  // split-K slabs (gemm_partial_floats)
   int* counters = nullptr;   // split-K arrival tickets, zero-initialised (gemm_counter_slots)
   const void* zeros = nullptr;  // >= 256 zero bytes (padded / out-of-range chunks; conv_wres: a null bias)
+  LnPtrs ln;
 };
 
 // Workspace needed by a GEMM with the chosen split-K (0 when not split).
@@ -108,7 +136,7 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 // at least min_tiles 256^2 tiles; SPI_GEMM_256_MIN, default 128, 0 = never).
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
 void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
-void gemm256_reload_env();  // re-read SPI_G256_PIPE
+void gemm256_reload_env();  // no knobs left (kept for spi_debug_gemm_reload_env)
 
 // Weight-resident 3x3/s1/p1 conv, 64 -> 64 channels, fp16 NHWC (conv_wres.hip): the
 // folded weights stay in LDS while a workgroup walks bands of output rows; gemm()
@@ -116,7 +144,7 @@ void gemm256_reload_env();  // re-read SPI_G256_PIPE
 bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p);
 void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
 void conv_wres_reload_env();
-void attention_reload_env();  // re-read SPI_ATTN_SWAP
+void attention_reload_env();  // no knobs left
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,

@@ -162,6 +162,36 @@ def test_vit_small_seq197(spi, zoo, gpu, prec):
     assert err < TOL[prec]
 
 
+@pytest.mark.parametrize("family", ["bert", "vit"])
+def test_transformer_layernorm_fold(spi, zoo, gpu, family, monkeypatch):
+    """The LayerNorm fold (ln_fold.hpp, DESIGN.md 3.6: statistics from the producing GEMM's
+    epilogue, gain folded into the consuming GEMM's weights, post-LN residuals recomputed
+    element-wise) against the separate LayerNorm launches (SPI_LN_FOLD=0) and the oracle; the
+    folded forward runs at most two LayerNorm launches."""
+    rng = np.random.default_rng(13)
+    if family == "bert":
+        m = zoo.bert(layers=3, init_std=0.05)
+        ids, mask = bert_inputs(rng, 3, 80, pad_from=50)
+        inputs, kw = [ids, mask], dict(max_batch=3, seq_len=128)
+    else:
+        m = zoo.vit(image=224, patch=16, layers=3, heads=2, dim=128, mlp_dim=256)
+        inputs, kw = [image(rng, 2, 224)], dict(max_batch=2)
+    ref = cpu_inference(m, inputs)[0]
+    rep = spi.ModelReplica(m, 0, "fp16", **kw)
+    folded = hip_forward(spi, rep, inputs, ref.shape, graphs=True)
+    ins = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in inputs]
+    out = torch.empty(ref.shape, device="cuda")
+    ops = rep.profile(ins, out, torch.cuda.current_stream().cuda_stream)
+    n_ln = sum(1 for o in ops if o["name"].startswith("layernorm"))
+    monkeypatch.setenv("SPI_LN_FOLD", "0")
+    plain = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), inputs, ref.shape)
+    d = normalized_max_error(folded, plain)
+    e_f, e_p = normalized_max_error(folded, ref), normalized_max_error(plain, ref)
+    print(f"{family} LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e}), LN launches {n_ln}")
+    assert n_ln <= 2
+    assert e_f < TOL["fp16"] and d < TOL["fp16"]
+
+
 def test_affine_codelet_like_reference(spi, gpu):
     """x + 1.5 on {1,2,3} (tests/unit/core/unit_starpu_setup.cpp:2332-2433)."""
     rep = spi.ModelReplica(None, 0, "fp32", max_batch=3, family="affine", affine=(1.0, 1.5))

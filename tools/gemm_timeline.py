@@ -4,7 +4,8 @@ build (s_memrealtime at entry, k-loop start, k-loop end and exit; HW_ID / XCC_ID
 
 For every gemm_kernel op of one ResNet-18 forward (the headline's replica, eager), the op is
 launched `reps` times back to back on worker 0's stream (Model::profile_op) -- isolated, and
-with the other workers replaying forwards (--loaded) -- and the last launch's stamps are read:
+with the other workers replaying forwards (--loaded; only the profiling thread's launches stamp)
+-- and the last launch's stamps are read:
 
   span      first entry -> last exit (the launch as the GPU runs it)
   skew      first entry -> last entry (dispatch of the grid)
