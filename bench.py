@@ -465,6 +465,32 @@ def config_line(spi, zoo, rtmod, name, batch, precision, workers, streams, steps
     return out
 
 
+def single_process_e2e(spi, zoo, rtmod, args, model, replica, world):
+    """One mini-runtime over replicas on devices 0..world-1 (this process), the same closed-loop
+    bs8 workload as `e2e` at 8 in flight per worker per device."""
+    reps = [replica] + [spi.ModelReplica(model, d, args.precision, max_batch=args.batch,
+                                         seq_len=128 if args.model.startswith("bert") else 0, graphs=True)
+                        for d in range(1, world)]
+    host_inputs, out_shape = make_inputs(args.model, args.batch, np.random.default_rng(11))
+    in_specs = ([((x.shape[1],), np.int64) for x in host_inputs] if args.model.startswith("bert")
+                else [((3, 224, 224), np.float32)])
+    rt = rtmod.Runtime(reps, in_specs, [(int(np.prod(out_shape[1:])), np.float32)], max_batch=args.batch,
+                       workers_per_device=args.workers, warmup_batches=-1)
+    inflight = 8 * args.workers * world
+    r = rt.loadgen(host_inputs, requests=args.e2e_requests * world, inflight=inflight, warmup=2 * inflight)
+    wt = rt.worker_times()  # workers are numbered device-major, args.workers per device
+    tasks_per_device = [sum(w["tasks"] for w in wt[d * args.workers:(d + 1) * args.workers]) for d in range(world)]
+    h2d = rt.h2d_mode
+    rt.close()
+    del reps[1:]
+    return {"value": round(r["inferences_per_s"], 2), "unit": "inferences/s", "devices": world,
+            "p50_latency_ms": round(r["p50_ms"], 4), "p99_latency_ms": round(r["p99_ms"], 4),
+            "requests": r["completed"], "failed": r["failed"], "inflight": inflight, "h2d_mode": h2d,
+            "tasks_per_device": tasks_per_device,
+            "shape": "one process, one runtime: one eager queue + one batcher over every device's workers "
+                     "(StarPU's single-process layout); value = inferences / (last response - first request)"}
+
+
 def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -653,6 +679,16 @@ def main():
                                      inflight=4 * args.workers, workers=args.workers), world, dist)
     result["e2e_half_load"] = {k: half[k] for k in ("value", "unit", "p50_latency_ms", "p95_latency_ms",
                                                     "p99_latency_ms", "requests", "inflight")}
+    # The reference's single-process serving shape (starpu_setup.cpp:388-432, inference_runner.cpp:
+    # 251-275): ONE runtime over every GPU's replica -- one eager queue, one batcher, the host staging
+    # of all devices in one process -- driven by one client loop; rank 0 runs it over devices
+    # 0..N-1 while the other ranks wait, so a SCALE run measures the shared-queue path too.
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        result["e2e_single_process"] = single_process_e2e(spi, zoo, rtmod, args, model, replica, world)
+    if world > 1:
+        dist.barrier()
     e2e1 = h.serial_e2e(40)
     result["p50_serial_e2e_latency_ms"] = round(percentile(e2e1, 50), 4)
 

@@ -169,6 +169,32 @@ def test_runtime_two_replicas_on_one_device(spi, zoo, rtmod):
     rt.close()
 
 
+def test_runtime_single_process_multi_device_adaptive(spi, zoo, rtmod):
+    """bench.py's single-process serving leg (`e2e_single_process`: one runtime over every
+    device's replica, one eager queue, one batcher -- StarPU's shape, starpu_setup.cpp:388-432,
+    inference_runner.cpp:251-275) rehearsed with device_ids [0, 0] under the adaptive batcher:
+    bs1 requests merged into tasks of up to 8, every request's row checked against the oracle,
+    both replicas' workers serving."""
+    m = zoo.resnet18(image=64)
+    reps = spi.clone_model_to_gpus(m, [0, 0], precision="fp16m", max_batch=8, image_size=64, graphs=True)
+    b = rtmod.batching_config("adaptive", 1, 8, coalesce_timeout_us=300, congestion=True, tick_us=500,
+                              entry_horizon_us=2000, exit_horizon_us=5000)
+    rt = rtmod.Runtime(reps, [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=2,
+                       batching=b)
+    rng = np.random.default_rng(21)
+    xs = rng.random((96, 3, 64, 64), dtype=np.float32)
+    ys = [np.full((1, 1000), np.nan, dtype=np.float32) for _ in range(96)]
+    for rid in range(96):
+        rt.submit(rid, [xs[rid:rid + 1]], [ys[rid]])
+    rt.drain()
+    assert rt.stats() == (96, 0)
+    ref = cpu_inference(m, [xs])[0]
+    assert normalized_max_error(np.concatenate(ys), ref) < 1e-3  # fp16m at 64x64 (resnet_tol: plain-fp16 bound 3e-3)
+    assert {c.worker_id for c in rt.completions} & {0, 1} and {c.worker_id for c in rt.completions} & {2, 3}
+    assert max(c.task_jobs for c in rt.completions) > 1  # the batcher merged requests
+    rt.close()
+
+
 @pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy", "worker_sdma"])
 def test_runtime_pipeline_with_small_slot_pool(spi, zoo, rtmod, h2d_mode):
     """Pipeline depth 3 per worker over a 2-slot pool (fewer slots than workers x depth): the
