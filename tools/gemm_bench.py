@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--epi-variants", action="store_true", help="with --model-epi: GELU launches also without GELU")
     ap.add_argument("--batch", type=int, default=0, help="override the conv batch (ResNet-152 bs32: 32)")
     ap.add_argument("--envs", default="", help="';'-separated knob sets KEY=VAL[&KEY=VAL] to sweep "
-                                               "(e.g. 'SPI_CONV_WRES=0;SPI_CONV_WRES_BPW=2')")
+                                               "(e.g. 'SPI_CONV_WRES=0;SPI_GEMM_MAXSPLIT=1')")
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
@@ -107,7 +107,7 @@ def main():
             print(f"{label}  {ms*1e3:8.2f} us  {fl/ms/1e9:8.1f} TF/s  [{plan or 'auto'}]", flush=True)
         os.environ["SPI_GEMM_PLAN"] = ""
         os.environ["SPI_GEMM_HALO_CFG"] = ""
-        for k in ("SPI_CONV_WRES", "SPI_CONV_WRES_BPW"):
+        for k in ("SPI_CONV_WRES", "SPI_GEMM_MAXSPLIT"):
             os.environ.pop(k, None)
         ops.lib.spi_debug_gemm_reload_env()
     dt = ops.act_dtype(a.prec)

@@ -20,9 +20,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KNOBS = ["SPI_STEM_FUSED", "SPI_STEM_PR", "SPI_GEMM_256_MIN", "SPI_GEMM_POLICY", "SPI_GEMM_HALO_CFG", "SPI_GEMM_MAXSPLIT", "SPI_GEMM_HALO_MINH", "SPI_GEMM_HALO", "SPI_GEMM_PAIR", "SPI_GEMM_BIG",
-         "SPI_GEMM_HALO_STAGES", "SPI_GEMM_XCD2D", "SPI_GEMM_STAGES", "SPI_GEMM_PLAN", "SPI_CONV_WRES",
-         "SPI_CONV_WRES_BPW", "SPI_CONV_WRES_NBUF", "SPI_CONV_WRES_WLA", "SPI_G256_PIPE", "SPI_GEMM_SPLIT_LOCAL", "SPI_GEMM_PAIR_JOINT", "SPI_GEMM_ST3_MIN", "SPI_GEMM_ST4_MIN", "SPI_GEMM_NO128SQ", "SPI_GEMM_SPLIT128", "SPI_GEMM_SQ_STAGES", "SPI_ATTN_SWAP", "SPI_GEMM_256_LONGK", "SPI_GEMM_DENSE_LONGK_T"]
+KNOBS = ["SPI_STEM_FUSED", "SPI_GEMM_256_MIN", "SPI_GEMM_256_LONGK", "SPI_GEMM_POLICY", "SPI_GEMM_HALO_CFG",
+         "SPI_GEMM_MAXSPLIT", "SPI_GEMM_PLAN", "SPI_CONV_WRES", "SPI_LN_FOLD"]
 
 
 def parse(p):

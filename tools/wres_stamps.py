@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Phase cycles of the weight-resident layer-1 conv (conv_wres.hip) from the s_memtime
 diagnostic build: tools/build_variant.sh tools/libspi_wres_stamps.so WORKTREE -DSPI_WRES_STAMPS
-then  python tools/wres_stamps.py tools/libspi_wres_stamps.so [bpw ...].
-Per workgroup: W + halo landed (band 0), compute, epilogue; the same for band 1; total;
+then  python tools/wres_stamps.py tools/libspi_wres_stamps.so.
+Per workgroup (one band each since round 4): W + halo landed, compute, epilogue; total;
 the shader clock from s_memtime / s_memrealtime (100 MHz).  Medians over workgroups."""
 import ctypes as C
 import os
@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 lib = C.CDLL(sys.argv[1])
-bpws = [int(x) for x in sys.argv[2:]] or [1, 2]
+bpws = [1]  # one band per workgroup (the multi-band variants were removed in round 4)
 V = C.c_void_p
 lib.spi_op_conv2d.argtypes = [C.c_int32, V, C.c_int32, C.c_int32, C.c_int32, C.c_int32, V, C.c_int32, C.c_int32,
                               C.c_int32, C.c_int32, C.c_int32, V, V, V, C.c_int32, V, V]
@@ -33,8 +33,6 @@ bias = torch.zeros(64, device="cuda")
 ws = torch.zeros(lib.spi_op_workspace_bytes(), dtype=torch.uint8, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 for bpw in bpws:
-    os.environ["SPI_CONV_WRES_BPW"] = str(bpw)
-    lib.spi_debug_gemm_reload_env()
     for _ in range(20):
         lib.spi_op_conv2d(1, x.data_ptr(), B, H, H, 64, wp.data_ptr(), 64, 3, 3, 1, 1, bias.data_ptr(), None,
                           y.data_ptr(), 1, ws.data_ptr(), V(s))
