@@ -166,6 +166,8 @@ struct KArgs {
   FastDiv fd_split;      // / splits
   FastDiv fd_ohw, fd_ow;  // conv: output row m -> image, then row / column
   FastDiv fd_tiles;       // grouped launches: / tiles
+  FastDiv fd_period, fd_hwp;  // halo kinds: / h_period, / h_hwp
+  int imgs;                   // conv: images (M / (OH * OW))
   // halo conv (kConvHalo): tile row block tm is the band of h_th "virtual" output
   // rows u in [tm * h_th, (tm + 1) * h_th) x the full width.  Virtual rows stack the
   // images with a period of h_period rows: image u / h_period, output row
@@ -449,17 +451,17 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   const int h_u0 = HALO ? tm * a.h_th : 0;
   if constexpr (HALO) {
     if (!a.h_off) {  // aligned band: contiguous output rows [m0, m_lim) of one image
-      const int img = h_u0 / a.h_period, oy0 = h_u0 - img * a.h_period;
+      const int img = fdiv(h_u0, a.fd_period), oy0 = h_u0 - img * a.h_period;
       m0 = (img * d.OH + oy0) * d.OW;
       m_lim = m0 + min(a.h_th, d.OH - oy0) * d.OW;
     }
   }
   [[maybe_unused]] auto halo_m = [&](int r) {
-    const int ty = r / d.OW, tx = r - ty * d.OW;
+    const int ty = fdiv(r, a.fd_ow), tx = r - ty * d.OW;
     const int u = h_u0 + ty;
-    const int img = u / a.h_period;
+    const int img = fdiv(u, a.fd_period);
     const int oy = u - img * a.h_period - a.h_off;
-    return (ty < a.h_th && img < d.M / (d.OH * d.OW) && (unsigned)oy < (unsigned)d.OH) ? (img * d.OH + oy) * d.OW + tx
+    return (ty < a.h_th && img < a.imgs && (unsigned)oy < (unsigned)d.OH) ? (img * d.OH + oy) * d.OW + tx
                                                                                       : -1;
   };
   const int kbeg = kslice * a.k_per_split;
@@ -543,19 +545,19 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   [[maybe_unused]] bool h_ok[HQ];
   [[maybe_unused]] int h_row[WTM_ / 16];
   if constexpr (HALO) {
-    const int imgs = d.M / (d.OH * d.OW);
+    const int imgs = a.imgs;
 #pragma unroll
     for (int q = 0; q < HQ; ++q) {
       const int p = (wave * HQ + q) * RPI + lane / CPR;
       const int c = slot ^ (p & (CPR - 1));
-      const int hy = p / a.h_hwp, hx = p - hy * a.h_hwp;
+      const int hy = fdiv(p, a.fd_hwp), hx = p - hy * a.h_hwp;
       int img, iy;
       if (a.h_off) {
         const int vy = h_u0 - 1 + hy;
-        img = vy < 0 ? imgs : vy / a.h_period;
+        img = vy < 0 ? imgs : fdiv(vy, a.fd_period);
         iy = vy - img * a.h_period - 1;
       } else {
-        img = h_u0 / a.h_period;
+        img = fdiv(h_u0, a.fd_period);
         iy = h_u0 - img * a.h_period - 1 + hy;
       }
       const int ix = hx - 1;
@@ -566,7 +568,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #pragma unroll
     for (int i = 0; i < WTM_ / 16; ++i) {
       const int r = (wave >> 1) * WTM_ + i * 16 + (lane & 15);
-      const int ty = r / d.OW, tx = r - ty * d.OW;
+      const int ty = fdiv(r, a.fd_ow), tx = r - ty * d.OW;
       h_row[i] = ty < a.h_th ? ty * a.h_hwp + tx : 0;
     }
   }
@@ -1700,6 +1702,7 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
   if (d.conv) {
     a.fd_ohw = make_fastdiv((unsigned)(d.OH * d.OW));
     a.fd_ow = make_fastdiv((unsigned)d.OW);
+    a.imgs = d.M / (d.OH * d.OW);
   }
   a.cin_shift = d.conv ? ilog2(d.Cin) : 0;
   a.kw_mul = (65536 + d.KW - 1) / d.KW;
@@ -1715,6 +1718,8 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
     a.h_hp = (pl.th + 2) * a.h_hwp;
     a.h_nblk = d.Cin / Traits<MODE>::ESTEP;
     a.h_bps = pl.bps;
+    a.fd_period = make_fastdiv((unsigned)std::max(1, pl.period));
+    a.fd_hwp = make_fastdiv((unsigned)a.h_hwp);
   }
   return a;
 }

@@ -8,7 +8,7 @@
 set -euo pipefail
 cfgs=("$@")
 if [ ${#cfgs[@]} -eq 0 ]; then
-  cfgs=(resnet18:8:fp16x3 bert_base:8:fp16 resnet152:32:fp16x3 vit_l_16:16:fp16)
+  cfgs=(resnet18:8:fp16m bert_base:8:fp16 resnet152:32:fp16x3 vit_l_16:16:fp16)
 fi
 for c in "${cfgs[@]}"; do
   IFS=: read -r model batch prec <<< "$c"

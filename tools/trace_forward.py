@@ -73,9 +73,9 @@ def main():
     h = bench.Harness(spi, rep, a.model, 0, a.batch, 1, np.random.default_rng(0))
     if a.ops_out:  # op names in launch order (one eager profiled forward; tools/pmc_traffic.py maps dispatches)
         import json
-        ops = rep.profile(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream)
+        rows = rep.launch_table(h.d_in[0], h.d_out[0], h.streams[0].cuda_stream)  # one entry per kernel launch
         with open(a.ops_out, "w") as f:
-            json.dump([o["name"] for o in ops], f)
+            json.dump([r["op"] for r in rows], f)
     rep.set_graphs(bool(a.graphs))
     for _ in range(a.iters):
         torch.cuda.synchronize()
