@@ -209,6 +209,10 @@ struct Job {
 struct Slot {
   std::vector<void*> h_in, h_out, d_in, d_out;
   hipEvent_t h2d = nullptr, done = nullptr;
+  // SPI_H2D_WORKER_SDMA: completion signal of this slot's SDMA copies (value = copies in
+  // flight) and its value word, which the worker stream waits on (hipStreamWaitValue64)
+  hsa_signal_t sig{};
+  volatile hsa_signal_value_t* sig_val = nullptr;
 };
 
 // SlotPoolBase::acquire / try_acquire / release (slot_pool_base.hpp:32-75).
@@ -220,7 +224,6 @@ struct SlotPool {
   std::condition_variable cv;
   hipStream_t copy_stream = nullptr;  // SPI_H2D_DEVICE_STREAM
   hsa_agent_t gpu_agent{}, cpu_agent{};  // SPI_H2D_WORKER_SDMA
-  uint32_t sdma_engine = 0;              // 0: ROCr assigns the engine; else the hsa_amd_sdma_engine_id_t bit
 
   int acquire() {
     std::unique_lock<std::mutex> lk(mu);
@@ -253,6 +256,7 @@ struct Task {
   int status = SPI_OK;
   std::string err;
   int64_t cs = 0, ce = 0;
+  bool sdma_pending = false;  // its SDMA copies were waited on the device only
 };
 
 struct Worker {
@@ -263,7 +267,6 @@ struct Worker {
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // H2D stream (may be the pool's shared one)
   bool own_copy_stream = false;
-  hsa_signal_t h2d_signal{};  // SPI_H2D_WORKER_SDMA: completion of the task's SDMA copies
   std::deque<Task> inflight;
   std::deque<Job> fixed;  // jobs pinned to this worker (under the runtime mutex)
   std::thread thread;
@@ -360,12 +363,9 @@ bool find_hsa_agents(int device, hsa_agent_t& gpu, hsa_agent_t& cpu) {
   return it->second.ok;
 }
 
-// One host -> device SDMA copy: on the pool's pinned engine when one was chosen
-// (SPI_H2D_SDMA_ENGINE), else on the engine ROCr assigns.
+// One host -> device SDMA copy on the engine ROCr assigns (pinning one engine measured no
+// different, round 3).
 hsa_status_t sdma_h2d(const SlotPool& pl, void* dst, const void* src, size_t bytes, hsa_signal_t sig) {
-  if (pl.sdma_engine)
-    return hsa_amd_memory_async_copy_on_engine(dst, pl.gpu_agent, src, pl.cpu_agent, bytes, 0, nullptr, sig,
-                                               (hsa_amd_sdma_engine_id_t)pl.sdma_engine, true);
   return hsa_amd_memory_async_copy(dst, pl.gpu_agent, src, pl.cpu_agent, bytes, 0, nullptr, sig);
 }
 
@@ -377,9 +377,12 @@ struct spi_runtime {
   std::vector<std::unique_ptr<SlotPool>> pools;
   std::vector<std::unique_ptr<Worker>> workers;
   std::unique_ptr<CopyPool> copier;
-  // SPI_H2D_SDMA_WAIT=blocked: the worker thread sleeps on the SDMA completion signal
-  // instead of polling it (read at create)
-  bool sdma_wait_blocked = false;
+  // SPI_H2D_WORKER_SDMA: the worker STREAM waits for the copies (hipStreamWaitValue64 on the
+  // slot signal's value word) and the thread moves on -- StarPU orders a task's transfers
+  // before its codelet without blocking the submitter (slot_manager_component.cpp:222-293).
+  // False when the device cannot (checked at create) or SPI_H2D_SDMA_WAIT=host: the worker
+  // thread waits on the signal before enqueueing the codelet (round 3).
+  bool sdma_stream_wait = false;
   // SPI_RT_COMPLETION=spin: finalize polls the completion event (yielding) instead of
   // hipEventSynchronize (read at create)
   bool spin_completion = false;
@@ -501,28 +504,42 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
   if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
     // SDMA engine copies (HIP's own hipMemcpyAsync takes a shader copy kernel for a
     // share of these 4.8 MB copies, 256 workgroups for ~120 us each, competing with
-    // the forwards: DESIGN.md 5.1), waited here; the slot's HBM buffers are free (the
-    // slot was released after its last task's completion event)
+    // the forwards: DESIGN.md 5.1); the slot's HBM buffers are free (the slot was
+    // released after its last task's completion event), so is its signal
     const SlotPool& pl = *pools[w->pool];
-    hsa_signal_store_screlease(w->h2d_signal, ni);
+    hsa_signal_store_screlease(slot.sig, ni);
     for (int i = 0; i < ni; ++i)
-      if (sdma_h2d(pl, slot.d_in[i], slot.h_in[i], (size_t)t.total * in_sample_bytes[i], w->h2d_signal) !=
+      if (sdma_h2d(pl, slot.d_in[i], slot.h_in[i], (size_t)t.total * in_sample_bytes[i], slot.sig) !=
           HSA_STATUS_SUCCESS) {
         t.status = SPI_ERR_DEVICE;
         t.err = "SDMA H2D copy failed";
-        hsa_signal_subtract_screlease(w->h2d_signal, ni - i);
+        hsa_signal_subtract_screlease(slot.sig, ni - i);
         break;
       }
-    // A wait may return before the condition holds (the HSA spec allows it;
-    // ROCclr loops too): wait until the value drops below 1.  Each completed copy
-    // decrements it; a failed copy leaves it negative.
-    hsa_signal_value_t v = hsa_signal_load_scacquire(w->h2d_signal);
-    while (v >= 1)
-      v = hsa_signal_wait_scacquire(w->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                    sdma_wait_blocked ? HSA_WAIT_STATE_BLOCKED : HSA_WAIT_STATE_ACTIVE);
-    if (v < 0 && t.status == SPI_OK) {
-      t.status = SPI_ERR_DEVICE;
-      t.err = "SDMA H2D failed";
+    if (sdma_stream_wait) {
+      // the codelet runs behind the copies on the device; finalize_oldest checks the signal
+      if (hipStreamWaitValue64(w->stream, (void*)slot.sig_val, 0, hipStreamWaitValueEq, ~0ull) != hipSuccess) {
+        hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
+        while (v >= 1) v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                     HSA_WAIT_STATE_ACTIVE);
+        if (v < 0 && t.status == SPI_OK) {
+          t.status = SPI_ERR_DEVICE;
+          t.err = "SDMA H2D failed";
+        }
+      } else {
+        t.sdma_pending = true;
+      }
+    } else {
+      // A wait may return before the condition holds (the HSA spec allows it;
+      // ROCclr loops too): wait until the value drops below 1.  Each completed copy
+      // decrements it; a failed copy leaves it negative.
+      hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
+      while (v >= 1)
+        v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+      if (v < 0 && t.status == SPI_OK) {
+        t.status = SPI_ERR_DEVICE;
+        t.err = "SDMA H2D failed";
+      }
     }
   }
   for (int i = 0; i < ni && t.status == SPI_OK && cfg.h2d_mode != SPI_H2D_WORKER_SDMA; ++i)
@@ -612,6 +629,20 @@ void spi_runtime::finalize_oldest(Worker* w) {
   SlotPool& pool = *pools[w->pool];
   Slot& slot = pool.slots[t.slot];
   const int64_t e0 = now_ns();
+  if (t.sdma_pending) {
+    // the stream waits for this slot's signal to reach 0; a failed copy leaves it negative:
+    // fail the task and release the stream (it runs the codelet on stale inputs, reported failed)
+    hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
+    while (v >= 1)
+      v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    if (v < 0) {
+      hsa_signal_store_screlease(slot.sig, 0);
+      if (t.status == SPI_OK) {
+        t.status = SPI_ERR_DEVICE;
+        t.err = "SDMA H2D failed";
+      }
+    }
+  }
   hipError_t se;
   if (spin_completion) {
     while ((se = hipEventQuery(slot.done)) == hipErrorNotReady) std::this_thread::yield();
@@ -694,7 +725,7 @@ void spi_runtime::destroy_resources() {
   for (auto& w : workers) {
     (void)hipSetDevice(w->device);
     if (w->own_copy_stream && w->copy_stream) (void)hipStreamDestroy(w->copy_stream);
-    if (w->h2d_signal.handle) (void)hsa_signal_destroy(w->h2d_signal);
+
     if (w->stream) (void)hipStreamDestroy(w->stream);
   }
   for (auto& p : pools) {
@@ -706,6 +737,7 @@ void spi_runtime::destroy_resources() {
       for (void* x : s.d_out) (void)hipFree(x);
       if (s.h2d) (void)hipEventDestroy(s.h2d);
       if (s.done) (void)hipEventDestroy(s.done);
+      if (s.sig.handle) (void)hsa_signal_destroy(s.sig);
     }
     if (p->copy_stream) (void)hipStreamDestroy(p->copy_stream);
   }
@@ -893,23 +925,10 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       rt->pools.push_back(std::move(pool));
       return cleanup_fail("no HSA agents for device " + std::to_string(c->device_ids[dv]));
     }
-    if (ok && cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
-      // SPI_H2D_SDMA_ENGINE: "high" = the highest engine free for host -> device copies, N =
-      // engine N, unset = ROCr's choice (shared with HIP's own copies)
-      if (const char* e = std::getenv("SPI_H2D_SDMA_ENGINE"); e && *e) {
-        uint32_t mask = 0;
-        if (hsa_amd_memory_copy_engine_status(pool->gpu_agent, pool->cpu_agent, &mask) == HSA_STATUS_SUCCESS && mask) {
-          if (std::strcmp(e, "high") == 0) {
-            pool->sdma_engine = 1u << (31 - __builtin_clz(mask));
-          } else {
-            const int n = std::atoi(e);
-            if (n >= 0 && n < 16 && (mask >> n) & 1u) pool->sdma_engine = 1u << n;
-          }
-        }
-        std::fprintf(stderr, "spi_runtime: device %d H2D SDMA engines free 0x%x, using 0x%x\n", pool->device, mask,
-                     pool->sdma_engine);
-      }
-    }
+    if (ok && cfg.h2d_mode == SPI_H2D_WORKER_SDMA)
+      for (Slot& sl : pool->slots)
+        ok = ok && hsa_signal_create(0, 0, nullptr, &sl.sig) == HSA_STATUS_SUCCESS &&
+             hsa_amd_signal_value_pointer(sl.sig, &sl.sig_val) == HSA_STATUS_SUCCESS;
     rt->pools.push_back(std::move(pool));
     if (!ok) return cleanup_fail("slot pool allocation failed on device " + std::to_string(c->device_ids[dv]));
     for (int k = 0; k < cfg.workers_per_device; ++k) {
@@ -924,8 +943,6 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
       } else if (cfg.h2d_mode == SPI_H2D_WORKER_COPY) {
         wok = wok && hipStreamCreateWithFlags(&w->copy_stream, hipStreamNonBlocking) == hipSuccess;
         w->own_copy_stream = true;
-      } else if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
-        wok = wok && hsa_signal_create(0, 0, nullptr, &w->h2d_signal) == HSA_STATUS_SUCCESS;
       }
       rt->workers.push_back(std::move(w));
       if (!wok) return cleanup_fail("stream creation failed for worker " + std::to_string(wid - 1));
@@ -950,13 +967,12 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
         const size_t bytes = rt->in_sample_bytes[i] * (size_t)cfg.max_batch;
         std::memset(sl.h_in[i], 0, bytes);
         if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
-          hsa_signal_store_screlease(w0->h2d_signal, 1);
-          if (sdma_h2d(pl, sl.d_in[i], sl.h_in[i], bytes, w0->h2d_signal) != HSA_STATUS_SUCCESS)
+          hsa_signal_store_screlease(sl.sig, 1);
+          if (sdma_h2d(pl, sl.d_in[i], sl.h_in[i], bytes, sl.sig) != HSA_STATUS_SUCCESS)
             return cleanup_fail("SDMA warm-up copy failed on device " + std::to_string(pl.device));
-          hsa_signal_value_t v = hsa_signal_load_scacquire(w0->h2d_signal);
+          hsa_signal_value_t v = hsa_signal_load_scacquire(sl.sig);
           while (v >= 1)
-            v = hsa_signal_wait_scacquire(w0->h2d_signal, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                          HSA_WAIT_STATE_ACTIVE);
+            v = hsa_signal_wait_scacquire(sl.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
           if (v < 0) return cleanup_fail("SDMA warm-up copy failed on device " + std::to_string(pl.device));
         } else if (hipMemcpyAsync(sl.d_in[i], sl.h_in[i], bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
           return cleanup_fail("H2D warm-up copy failed on device " + std::to_string(pl.device));
@@ -991,7 +1007,23 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   }
   rt->warmup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - warm_t0).count();
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
-  if (const char* e = std::getenv("SPI_H2D_SDMA_WAIT"); e && std::strcmp(e, "blocked") == 0) rt->sdma_wait_blocked = true;
+  if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
+    // the worker streams wait for the copies unless SPI_H2D_SDMA_WAIT=host (A/B) or the device
+    // refuses the wait: one on an already-satisfied value word per worker stream first
+    const char* e = std::getenv("SPI_H2D_SDMA_WAIT");
+    rt->sdma_stream_wait = !(e && std::strcmp(e, "host") == 0);
+    for (auto& w : rt->workers) {
+      if (!rt->sdma_stream_wait) break;
+      (void)hipSetDevice(w->device);
+      Slot& sl = rt->pools[w->pool]->slots[0];
+      hsa_signal_store_screlease(sl.sig, 0);
+      if (hipStreamWaitValue64(w->stream, (void*)sl.sig_val, 0, hipStreamWaitValueEq, ~0ull) != hipSuccess ||
+          hipStreamSynchronize(w->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        rt->sdma_stream_wait = false;
+      }
+    }
+  }
   if (const char* e = std::getenv("SPI_RT_COMPLETION"); e && std::strcmp(e, "spin") == 0) rt->spin_completion = true;
   rt->last_target = cfg.max_batch;
   for (auto& w : rt->workers) w->thread = std::thread(&spi_runtime::run, rt.get(), w.get());
