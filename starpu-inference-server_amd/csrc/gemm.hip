@@ -1515,6 +1515,15 @@ Knobs& knobs() {
   return k;
 }
 
+// gemm256 routing by desc (gemm() also needs 16-byte aligned A / W) and its split-K
+bool routes_256(const GemmDesc& d, Prec prec) {
+  const Knobs& k = knobs();
+  return prec == Prec::F16 && (gemm256_eligible(d, prec, k.g256_min) ||
+                               (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k &&
+                                gemm256_eligible(d, prec, k.g256_longk_tiles)));
+}
+int g256_splits(const GemmDesc& d) { return gemm256_splits(d, knobs().target, knobs().max_split); }
+
 Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   const Knobs& k = knobs();
   if (k.max_split) pl.splits = std::min(pl.splits, k.max_split);
@@ -1838,16 +1847,21 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
 
 }  // namespace
 
+// Workspace of the general kernel's plan, or of gemm256's when gemm() may route the desc
+// there (routing also needs 16-byte aligned A / W, unknown here: the larger of the two).
 size_t gemm_partial_floats(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
-  if (pl.splits <= 1) return 0;
-  return (size_t)plan_tiles(d, pl) * pl.splits * pl.bm * pl.bn;
+  size_t f = pl.splits <= 1 ? 0 : (size_t)plan_tiles(d, pl) * pl.splits * pl.bm * pl.bn;
+  if (routes_256(d, prec) && g256_splits(d) > 1)
+    f = std::max(f, (size_t)((d.M + 255) / 256) * (d.N / 256) * g256_splits(d) * 256 * 256);
+  return f;
 }
 
 size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
-  if (pl.splits <= 1) return 0;
-  return 2 * (size_t)plan_tiles(d, pl);  // per tile: arrival ticket + published-slab count
+  size_t n = pl.splits <= 1 ? 0 : 2 * (size_t)plan_tiles(d, pl);  // per tile: arrival ticket + published-slab count
+  if (routes_256(d, prec) && g256_splits(d) > 1) n = std::max(n, 2 * (size_t)((d.M + 255) / 256) * (d.N / 256));
+  return n;
 }
 
 int gemm_kstep(Prec prec) { return estep_of(prec); }
@@ -1930,12 +1944,9 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
     case Prec::F16:
       if (conv_wres_eligible(d, prec, p))
         conv_wres(d, p, s);
-      else if ((gemm256_eligible(d, prec, knobs().g256_min) ||
-                (knobs().g256_longk_tiles > 0 && d.K >= knobs().g256_longk_k &&
-                 gemm256_eligible(d, prec, knobs().g256_longk_tiles))) &&
-               (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
-          (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
-        gemm256(d, p, s);
+      else if (routes_256(d, prec) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
+               (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
+        gemm256(d, p, g256_splits(d), s);
       else
         launch<(int)Prec::F16>(d, p, s);
       break;

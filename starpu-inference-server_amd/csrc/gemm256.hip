@@ -29,6 +29,7 @@
 #include "ln_fold.hpp"
 #include "spi_kernels.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
@@ -60,8 +61,16 @@ struct G256Args {
   const float* ln_c1;
   float* ln_out_stats;
   _Float16* c16;
+  // split-K (gemm256_splits): `splits` slices of `ktp` k-tiles; fp32 slabs [tile][slice][256 x 256]
+  // in fragment order and two counter words per tile (arrival ticket, published slabs)
+  int splits, ktp;
+  float* partial;
+  int* counters;
 };
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kMaxSplits = 4;     // split-K slices (gemm256_splits)
+constexpr int kMinSliceKt = 8;    // k-tiles per slice at least (ViT-L out-proj, K = 1024: 2 slices)
 constexpr int kBufBytes = 65536;  // one k-tile: A 256 x 128 B + B 256 x 128 B
 constexpr int kBOff = 32768;
 
@@ -112,17 +121,21 @@ __device__ __forceinline__ void bar() {
 template <int RES>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
+  __shared__ int s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // XCD-aware bijective remap: the workgroups one XCD receives get consecutive ids
-  const int nwg = g.tiles_m * g.tiles_n, orig = blockIdx.x;
+  // XCD-aware bijective remap: the workgroups one XCD receives get consecutive ids (slice-major:
+  // neighbours share a k-range of the same W panel)
+  const int tiles = g.tiles_m * g.tiles_n, nwg = tiles * g.splits, orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tm = wgid % g.tiles_m, tn = wgid / g.tiles_m;
+  const int slice = wgid / tiles, tile = wgid - slice * tiles;
+  const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int KT = g.K >> 6;
+  const int kt0 = slice * g.ktp;
+  const int KT = min(g.ktp, (g.K >> 6) - kt0);
 
   // per-lane DMA sources of each quarter's two pieces (k-tile 0); advance 128 B per k-tile
   const char* src[4][2];
@@ -137,10 +150,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
         const int r = base + rl;
         if (q == 0 || q == 3) {
           const int m = min(m0 + r, g.M - 1);  // rows past M: a valid row, never stored
-          src[q][j] = reinterpret_cast<const char*>(g.A + (size_t)m * g.lda) + chunk * 16;
+          src[q][j] = reinterpret_cast<const char*>(g.A + (size_t)m * g.lda + kt0 * 64) + chunk * 16;
           dsto[q][j] = base * 128;
         } else {
-          src[q][j] = reinterpret_cast<const char*>(g.W + (size_t)(n0 + r) * g.ldw) + chunk * 16;
+          src[q][j] = reinterpret_cast<const char*>(g.W + (size_t)(n0 + r) * g.ldw + kt0 * 64) + chunk * 16;
           dsto[q][j] = kBOff + base * 128;
         }
       }
@@ -249,6 +262,58 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (wr == 0) bar();  // the skew, closed
   }
 
+  if (g.splits > 1) {
+    // Split-K hand-off, gemm.hip's protocol (tickets first; slices that are not last publish
+    // their partial write-through (sc1) in fragment order -- thread tid's accumulator (a, b) is
+    // 16 contiguous bytes at ((a * 4 + b) * 512 + tid) * 16 -- drain, and count it in the second
+    // word; the last arriver polls the count, resets both words and reads the slabs with sc1
+    // loads).  Partials are summed in slice order whichever slice arrives last (((p0 + p1) + p2)
+    // + p3, the own partial from registers, slots past `splits` read as 0 through the buffer
+    // range): results do not depend on arrival order.
+    constexpr int SLAB = 256 * 256;
+    int* words = g.counters + 2 * tile;
+    float* slabs = g.partial + (size_t)tile * g.splits * SLAB;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(slabs, (short)0, g.splits * SLAB * 4, 0x00020000);
+    if (tid == 0) s_ticket = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_ticket < g.splits - 1) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
+                                                 (slice * SLAB + ((a * 4 + b) * 512 + tid) * 4) * 4, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid == 0) __hip_atomic_fetch_add(words + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g.splits - 1)
+        __builtin_amdgcn_s_sleep(1);
+      __hip_atomic_store(words, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(words + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      floatx4 v[kMaxSplits][4];
+#pragma unroll
+      for (int z = 0; z < kMaxSplits; ++z)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          v[z][b] = __builtin_bit_cast(
+              floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (z * SLAB + ((a * 4 + b) * 512 + tid) * 4) * 4, 0, 16));
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        floatx4 sum = slice == 0 ? acc[a][b] : v[0][b];
+#pragma unroll
+        for (int z = 1; z < kMaxSplits; ++z) sum += slice == z ? acc[a][b] : v[z][b];
+        acc[a][b] = sum;
+      }
+    }
+  }
+
   // Epilogue through LDS (the k-loop's buffers are free): per-element stores from the
   // fragment layout (2-4 bytes, 128 per lane) made the tail store-issue-bound -- as
   // long as the k-loop itself (cdna_hip_programming.md T21).  Two rounds, one per
@@ -325,8 +390,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias8[e] = 0.f;
   }
-  // activation and output format are dispatched once, outside the rounds
-  auto epi = [&](auto act_c, auto f32_c, auto guard_c) {
+  // activation and output format are dispatched once, outside the rounds (always_inline: left
+  // to itself hipcc outlined the 12 instances as calls, spilling the accumulators -- 944 bytes of
+  // scratch per thread -- around each)
+  auto epi = [&](auto act_c, auto f32_c, auto guard_c) __attribute__((always_inline)) {
     constexpr int ACT = decltype(act_c)::value;
     constexpr bool OUTF32 = decltype(f32_c)::value;
     constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
@@ -456,13 +523,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 };
-  auto by_guard = [&](auto act_c, auto f32_c) {
+  auto by_guard = [&](auto act_c, auto f32_c) __attribute__((always_inline)) {
     if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
       epi(act_c, f32_c, std::false_type{});
     else
       epi(act_c, f32_c, std::true_type{});
   };
-  auto by_act = [&](auto f32_c) {
+  auto by_act = [&](auto f32_c) __attribute__((always_inline)) {
     if (act == Act::Gelu)
       by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
     else if (act == Act::Relu)
@@ -480,6 +547,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 
 void gemm256_reload_env() {}
 
+int gemm256_splits(const GemmDesc& d, int target, int max_split) {
+  const int tiles = (d.M + 255) / 256 * (d.N / 256), kt = d.K / 64;
+  if (tiles >= target || max_split == 1) return 1;
+  int s = std::min({(target + tiles - 1) / tiles, kt / kMinSliceKt, kMaxSplits});
+  if (max_split > 0) s = std::min(s, max_split);
+  if (s <= 1) return 1;
+  const int ktp = (kt + s - 1) / s;
+  return (kt + ktp - 1) / ktp;
+}
+
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles) {
   if (min_tiles <= 0 || prec != Prec::F16 || d.conv || d.krep != 1 || d.a_split || d.out_split || d.pool_rows ||
       d.out_f16)
@@ -488,8 +565,10 @@ bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles) {
   return (d.M + 255) / 256 * (d.N / 256) >= min_tiles;
 }
 
-void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
+void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
   if (d.N % 256 || d.K % 64 || d.Kpad != d.K) throw std::invalid_argument("gemm256: N % 256, K % 64, Kpad == K");
+  if (splits < 1 || splits > kMaxSplits || (splits > 1 && (!p.partial || !p.counters)))
+    throw std::invalid_argument("gemm256: 1..4 split-K slices, with slabs and counters");
   G256Args g;
   g.A = static_cast<const _Float16*>(p.A);
   g.W = static_cast<const _Float16*>(p.W);
@@ -522,8 +601,14 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, hipStream_t s) {
   if ((d.ln_in_chunks > 0 || d.ln_out) && !g.vec_ok)
     throw std::invalid_argument("gemm256: the LayerNorm fold needs the vector epilogue");
   if (d.res_ln_chunks > 0) throw std::invalid_argument("gemm256: no residual LayerNorm (post-LN) epilogue");
+  const int kt = d.K / 64;
+  g.ktp = (kt + splits - 1) / splits;
+  g.splits = (kt + g.ktp - 1) / g.ktp;
+  if (g.splits != splits) throw std::invalid_argument("gemm256: splits must leave no empty slice");
+  g.partial = p.partial;
+  g.counters = p.counters;
   const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
-  const dim3 grid(g.tiles_m * g.tiles_n), blk(512);
+  const dim3 grid(g.tiles_m * g.tiles_n * g.splits), blk(512);
   if (res == 0)
     SPI_LAUNCH((gemm256_kernel<0>), grid, blk, 0, s, g);
   else if (res == 1)

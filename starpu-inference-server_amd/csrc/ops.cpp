@@ -15,7 +15,7 @@ namespace {
 
 constexpr size_t kZeroBytes = 256;
 constexpr size_t kTickets = 16384;
-constexpr size_t kSlabFloats = (size_t)8 << 20;  // 32 MiB of split-K slabs
+constexpr size_t kSlabFloats = (size_t)16 << 20;  // 64 MiB of split-K slabs (gemm256 at ViT-L FFN2: 40 MiB)
 
 bool prec_of(int32_t p, spi::Prec* out) {
   if (p == 0) *out = spi::Prec::F32;

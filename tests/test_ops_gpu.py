@@ -354,6 +354,37 @@ def test_gemm256_in_place_residual(ops, gemm256_everywhere, router, M, N, K):
         assert err < 1e-5, f"in-place gemm {M}x{N}x{K} ({router}): {err:.3e}"
 
 
+@pytest.mark.parametrize("maxsplit", ["1", "2", "3", "0"])
+@pytest.mark.parametrize("M,N,K,res", [(600, 512, 2048, "f32"), (3152, 1024, 1024, None), (257, 256, 1536, "f16")])
+def test_gemm256_split_k(ops, gemm256_everywhere, maxsplit, M, N, K, res):
+    """gemm256's split-K (grids under 128 workgroups: slices of >= 8 k-tiles, at most 4; the
+    last slice to arrive sums the write-through slabs in slice order).  SPI_GEMM_MAXSPLIT caps
+    the slices (0 = uncapped: 4 for 600x512x2048, slices of 8 k-tiles; 3 gives a short last
+    slice).  The sum order does not depend on arrival: two launches agree bit for bit."""
+    import os
+    os.environ["SPI_GEMM_MAXSPLIT"] = maxsplit
+    ops.lib.spi_debug_gemm_reload_env()
+    try:
+        g = torch.Generator().manual_seed(M + 7 * N + K)
+        A = torch.randn(M, K, generator=g).half()
+        W = torch.randn(N, K, generator=g) / K ** 0.5
+        b = torch.randn(N, generator=g)
+        R = None if res is None else torch.randn(M, N, generator=g)
+        if res == "f16":
+            R = R.half()
+        ref = A.float() @ W.half().float().T + b + (0 if R is None else R.float())
+        Wp = ops.pack_weight("fp16", W)
+        outs = [ops.gemm("fp16", A.cuda(), Wp, N, bias=b.cuda(), residual=None if R is None else R.cuda(),
+                         out_f32=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        err = normalized_max_error(outs[0].cpu().numpy(), ref.numpy())
+        assert err < 1e-5, f"gemm256 split-K {M}x{N}x{K} (max {maxsplit}): {err:.3e}"
+        assert torch.equal(outs[0], outs[1]), "split-K sums depend on arrival order"
+    finally:
+        os.environ.pop("SPI_GEMM_MAXSPLIT", None)
+        ops.lib.spi_debug_gemm_reload_env()
+
+
 def test_gemm256_unaligned_output(ops, gemm256_everywhere):
     """An output buffer off 16-byte alignment takes gemm256's per-element epilogue."""
     M, N, K = 300, 512, 128
