@@ -1110,6 +1110,11 @@ int32_t spi_runtime_h2d_mode(const spi_runtime* rt) { return rt ? rt->cfg.h2d_mo
 
 double spi_runtime_warmup_seconds(const spi_runtime* rt) { return rt ? rt->warmup_s : 0.0; }
 
+int32_t spi_runtime_h2d_device_wait(const spi_runtime* rt) {
+  if (!rt || rt->cfg.h2d_mode != SPI_H2D_WORKER_SDMA) return -1;
+  return rt->sdma_stream_wait ? 1 : 0;
+}
+
 int32_t spi_runtime_batch_target(const spi_runtime* rt) {
   if (!rt) return 0;
   std::lock_guard<std::mutex> lk(const_cast<spi_runtime*>(rt)->mu);
