@@ -179,6 +179,7 @@ struct KArgs {
   // padding around) form an h_hwp-wide halo image of h_hp pixels; h_nblk channel
   // blocks, h_bps of them per split-K slice
   int h_th, h_period, h_off, h_hwp, h_hp, h_nblk, h_bps;
+  int win_nblk_shift;  // window kind (kConvTapW): log2 of the channel blocks per tap
   int splits;  // split-K slices (the grid holds tiles x splits workgroups of this problem)
 #ifdef SPI_GEMM_TIMELINE
   int tl;  // stamp this launch (tools/gemm_timeline.py)
@@ -287,6 +288,17 @@ __device__ __forceinline__ void glds16(const void* src, char* dst) {
                : "memory");
 }
 
+// The 4-byte form (a 256-byte piece: lane l's 4 bytes to dst + 4 l), same hand-counted contract.
+__device__ __forceinline__ void glds4(const void* src, char* dst) {
+  const lds_ptr_t lp = (lds_ptr_t)dst;
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lp);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(m0v)
+               : "memory");
+}
+
 template <int RB>
 __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
   constexpr int CPR = RB / 16;  // 16-byte chunks per image row
@@ -297,7 +309,7 @@ __device__ __forceinline__ u32x4 rd_chunk(const char* img, int row, int c) {
 // k-step: scalar tap walk + per-row tap mask); conv in general (per-chunk taps:
 // the stem); 3x3/s1/p1 conv from an LDS-resident input band (kConvHalo, below).
 // Separate instantiations keep each kind's loop free of the others.
-enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS = 4 };
+enum : int { kDense = 0, kConvTap = 1, kConvGen = 2, kConvHalo = 3, kConvHaloS = 4, kConvTapW = 5 };
 
 // Split-K is compiled into the 64x64 and 128x64 tiles and the halo kinds (no plan
 // rule splits 128x128; the reducer costs 36-120 VGPRs there).  Launch bounds ask
@@ -322,9 +334,20 @@ template <int BM, int KIND, int NW>
 constexpr int kHaloHQ = KIND == kConvHaloS ? 3 : NW == 8 ? 6 : BM == 64 ? 4 : 8;
 template <int KIND>
 constexpr bool kIsHalo = KIND == kConvHalo || KIND == kConvHaloS;
+// kConvTapW (round 4): 3x3/s1/p1 tap walk with the three kw taps of a (kh, channel block)
+// reading one A window.  For stride 1 and padding 1 (OH = H, OW = W) the input pixel of tap
+// (kh, kw) of output row m is the global pixel m + (kh - 1) W + kw - 1, so the 64 rows of a
+// tile read, for the three kw taps, the 66 consecutive pixels from m0 + (kh - 1) W - 1 on:
+// one DMA'd window of kWinRows rows (2 x 16-byte pieces + 1 x 4-byte piece per wave: 72
+// rows) feeds 3 k-steps -- 9 KiB of A per 3 steps instead of 24 (a tile step's LDS ingest
+// 16 -> 11 KiB; the layer-2..4 convs run at the per-CU ingest ceiling).
+// Taps that fall into the padding read a real neighbour pixel of the window and are zeroed
+// at fragment read by the row's tap mask.  Only W goes through the STAGES ring.
+constexpr int kWinRows = 72;
 template <int BM, int BN, int STAGES, int KIND, int NW>
 constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND, NW> * NW * 8 * 128 + 16
-                                        : STAGES * (BM + BN) * 128 + 16;
+                          : KIND == kConvTapW ? STAGES * BN * 128 + 2 * kWinRows * 128 + 16
+                                              : STAGES * (BM + BN) * 128 + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
 // size per wave, capped by what the tile's LDS ring allows (NW / 4 waves per SIMD
 // per block, 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
@@ -343,6 +366,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
+  constexpr bool WIN = KIND == kConvTapW;
+  constexpr bool AR = !HALO && !WIN;  // A tiles go through the ring
+  static_assert(!WIN || (BM == 64 && BN == 64 && NW == 4 && STAGES == 3), "window kind: 64 x 64, 4 waves, 3 W stages");
   constexpr int NT = 64 * NW;  // threads per workgroup
   static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
   using TR = Traits<MODE>;
@@ -350,15 +376,16 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
   constexpr int CPR = RB / 16;             // chunks per image row
   constexpr int RPI = 64 / CPR;            // image rows per 1-KiB DMA instruction
-  constexpr int IMG = (HALO ? BN : BM + BN) * RB;  // bytes per ring stage (halo: W only)
+  constexpr int IMG = (AR ? BM + BN : BN) * RB;  // bytes per ring stage (halo, window: W only)
   constexpr int AQ = BM / RPI / NW, BQ = BN / RPI / NW;  // DMA instructions per wave per step
-  static_assert(HALO || AQ * RPI * NW == BM, "A image rows per wave");
+  static_assert(!AR || AQ * RPI * NW == BM, "A image rows per wave");
   static_assert(BQ * RPI * NW == BN, "W image rows per wave");
-  constexpr int QPS = (HALO ? 0 : AQ) + BQ;
+  constexpr int QPS = (AR ? AQ : 0) + BQ;
   constexpr int HQ = HALO ? kHaloHQ<BM, KIND, NW> : 1;  // halo DMA instructions per wave per block
-  constexpr int HBUF = HALO ? HQ * NW * RPI * RB : 0;  // bytes per halo buffer
+  constexpr int HBUF = HALO ? HQ * NW * RPI * RB : WIN ? kWinRows * RB : 0;  // bytes per halo / window buffer
   constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND, NW>;
   static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
+  static_assert(!WIN || RB == 128, "window rows are 128-byte pixel blocks");
   static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
   int* s_flag = reinterpret_cast<int*>(lds + LDSB - 16);
@@ -486,7 +513,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // inside the image (0 for rows past M).  Indexed by the unrolled q only.
   uint32_t a_mask[AQ];
 #pragma unroll
-  for (int q = 0; q < (HALO ? 0 : AQ); ++q) {
+  for (int q = 0; q < (AR ? AQ : 0); ++q) {
     const int r = (wave * AQ + q) * RPI + lane / CPR;
     a_koff[q] = (slot ^ (r & (CPR - 1))) * EPC;
     const int m = m0 + r;
@@ -582,6 +609,46 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       }
     }
   };
+  // Window kind: super-step j of the slice is global super-step w_g0 + j = (kh, channel block
+  // cb), kh-major (g = kh * nblk + cb); its k-step 3 j + kw reads W k-step (kh * 3 + kw) *
+  // nblk + cb (k = tap * Cin + c).  DMA side of a window: pieces 0, 1 of wave w (16 bytes a
+  // lane) fill rows 16 w + 8 q + lane / 8, slot lane & 7; piece 2 (4 bytes a lane) rows
+  // 64 + 2 w + lane / 32, slot (lane & 31) / 4 -- w_off: the source byte offset in the pixel's
+  // 128-byte block (chunk slot ^ (row & 7), the ring images' swizzle).
+  [[maybe_unused]] const int w_g0 = WIN ? kbeg / (3 * ESTEP) : 0;
+  [[maybe_unused]] const int w_nbs = WIN ? a.win_nblk_shift : 0;
+  [[maybe_unused]] int w_row[3], w_off[3];
+  if constexpr (WIN) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = wave * 16 + q * 8 + (lane >> 3);
+      w_row[q] = r;
+      w_off[q] = ((lane & 7) ^ (r & 7)) << 4;
+    }
+    const int r = 64 + wave * 2 + (lane >> 5);
+    w_row[2] = r;
+    w_off[2] = ((((lane & 31) >> 2) ^ (r & 7)) << 4) + ((lane & 3) << 2);
+  }
+  auto issue_win = [&](int jj, int buf) {
+    if constexpr (WIN) {
+      constexpr int PSH = __builtin_ctz(sizeof(AT));
+      const int g = w_g0 + jj, kh = g >> w_nbs, cb = g & ((1 << w_nbs) - 1);
+      const int p0 = m0 + (kh - 1) * d.W - 1;  // global pixel of window row 0
+      const char* base = reinterpret_cast<const char*>(Ap) + cb * RB;
+      char* dst = lds + STAGES * IMG + buf * HBUF;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int pix = p0 + w_row[q];
+        const char* src = (unsigned)pix < (unsigned)d.M ? base + ((size_t)pix << (a.cin_shift + PSH)) + w_off[q] : zeros;
+        if (q < 2)
+          glds16(SPI_A_SRC(src), dst + (wave * 2 + q) * 1024);
+        else
+          glds4(SPI_A_SRC(src), dst + 64 * RB + wave * 256);
+      }
+    }
+  };
+  [[maybe_unused]] int w_tap0 = 0, w_j = 0;  // the running super-step's kh * 3 and index
+
   // halo: scalar (block, tap) walk of the issued W steps; k = tap * Cin + c, so
   // step (blk, tap) is W k-step tap * nblk + blk
   int hw_blk = h_b0, hw_tap = 0;
@@ -616,6 +683,14 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         hw_tap = 0;
         ++hw_blk;
       }
+      return;
+    } else if constexpr (WIN) {
+      const int jj = step / 3, kw = step - jj * 3;
+      const int g = w_g0 + jj, kh = g >> w_nbs, cb = g & ((1 << w_nbs) - 1);
+      const int wstep = ((kh * 3 + kw) << w_nbs) + cb;
+#pragma unroll
+      for (int q = 0; q < BQ; ++q)
+        SPI_DMA_W((const void*)(b_src[q] + (size_t)wstep * RB), (lds_ptr_t)(dst + (wave * BQ + q) * 1024), 16, 0, 0);
       return;
     } else if constexpr (CONV) {
       if constexpr (TAP) {
@@ -688,6 +763,22 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // window kind: taps (bit kh * 3 + kw) inside the image for this lane's A fragment rows
+  [[maybe_unused]] uint32_t w_mask[TI];
+  if constexpr (WIN) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      uint32_t mask = 0u;
+      if (m < d.M) {
+        const int img = fdiv(m, a.fd_ohw), rem = m - img * (d.OH * d.OW);
+        const int oh = fdiv(rem, a.fd_ow), ow = rem - oh * d.OW;
+        const uint32_t cols = (ow > 0 ? 1u : 0u) | 2u | (ow + 1 < d.W ? 4u : 0u);
+        mask = (oh > 0 ? cols : 0u) | (cols << 3) | (oh + 1 < d.H ? cols << 6 : 0u);
+      }
+      w_mask[i] = mask;
+    }
+  }
 
   // Residual tile prefetch (64 x 64 tiles on the vector epilogue path): the epilogue's
   // residual loads were the last dependent memory round trip of a launch (~0.5-1 us of a
@@ -703,9 +794,12 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   [[maybe_unused]] const int res_rb = (MODE == kF16X3S || sizeof(typename TR::Out) == 4 || d.res_f32) ? 256 : 128;
   [[maybe_unused]] const int rpw = res_rb * BM / 1024 / NW;  // 2 or 4
   [[maybe_unused]] const bool rpf_tile = RPF && a.p.res && a.vec_ok && n0 + BN <= d.N && !d.pool_rows;
-  [[maybe_unused]] const bool rpf_loop = rpf_tile && a.splits == 1;  // prefetched inside the k-loop
+  // (window kind: into the window buffer the last super-step does not use -- 9 KiB, so fp16
+  // residual rows only -- and the tile parks at 0)
+  [[maybe_unused]] const bool rpf_loop = rpf_tile && a.splits == 1 && (!WIN || res_rb == 128);
   [[maybe_unused]] const int rpf_step = max(0, nsteps - STAGES + 1);
-  [[maybe_unused]] const int rpf_off = (nsteps % STAGES) * IMG;
+  [[maybe_unused]] const int rpf_off = WIN ? STAGES * IMG + ((nsteps / 3) & 1) * HBUF : (nsteps % STAGES) * IMG;
+  [[maybe_unused]] const int park_off = WIN ? 0 : ((nsteps - 1) % STAGES) * IMG;
   auto issue_res = [&](char* dst) {
     if constexpr (RPF) {
       const int rpp = 1024 / res_rb, cpr = res_rb / 16;  // rows per piece, 16-byte chunks per row
@@ -730,6 +824,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 
   SPI_RT(rt_p2);
   if constexpr (HALO) issue_halo(h_b0, 0);  // lands before W step 0 (in-order vmcnt)
+  if constexpr (WIN) issue_win(0, 0);
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) issue(s, s);
@@ -1073,6 +1168,28 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         dma_wait_barrier<G * BQ + HQ>();
       else
         dma_wait_barrier<G * BQ>();
+    } else if constexpr (WIN) {
+      // issue order: window j, ..., W(3j + 2) and window j + 1 at step 3j, W(3j + 3) at 3j + 1,
+      // W(3j + 4) at 3j + 2.  Step 3j needs window j and W(3j) (W(3j + 1) in flight), 3j + 1
+      // needs W(3j + 1) (W(3j + 2) and window j + 1 in flight), 3j + 2 needs W(3j + 2)
+      // (window j + 1 and W(3j + 3)); last_blk: no super-step follows.  The residual
+      // prefetch (issued at step 3j + 1 of the last super-step) stays in flight at 3j + 2.
+      constexpr int XQ = 3;  // window pieces per wave
+      if constexpr (TP == 0) {
+        dma_wait_barrier<BQ>();
+      } else if constexpr (TP == 1) {
+        if (last_blk)
+          dma_wait_barrier<BQ>();
+        else
+          dma_wait_barrier<BQ + XQ>();
+      } else {
+        if (!last_blk)
+          dma_wait_barrier<XQ + BQ>();
+        else if (RPF && rpf_loop)
+          dma_wait_barrier<2>();  // rpw = 2: 64 fp16 residual rows
+        else
+          dma_wait_barrier<0>();
+      }
     } else {
       // steps after the residual prefetch (rpf_loop, issued youngest at rpf_step) also leave
       // its rpw pieces in flight
@@ -1106,21 +1223,29 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     // All of this step's fragment reads go out first, then the next step's
     // DMAs (their issue cost overlaps the LDS latency), then the MFMAs.
     const char* As = lds + U * IMG;
-    const char* Bs = HALO ? As : As + BM * RB;
-    // A fragment i: image and row (halo: pixel of this tap, kh * (W + 2) + kw on)
-    const char* Ab = HALO ? Hs : As;
+    const char* Bs = AR ? As + BM * RB : As;
+    // A fragment i: image and row (halo: pixel of this tap, kh * (W + 2) + kw on; window:
+    // row + kw)
+    const char* Ab = AR ? As : Hs;
     [[maybe_unused]] const int toff = HALO ? (TP / 3) * a.h_hwp + TP % 3 : 0;
     auto arow = [&](int i) {
       if constexpr (HALO)
         return h_row[i] + toff;
+      else if constexpr (WIN)
+        return wm * WTM + i * 16 + fr + TP;
       else
         return wm * WTM + i * 16 + fr;
     };
+    // window kind: is tap (kh, TP) of fragment row i inside the image
+    [[maybe_unused]] auto tap_ok = [&](int i) { return ((w_mask[i] >> (w_tap0 + TP)) & 1u) != 0u; };
     auto issue_next = [&] {
       if constexpr (HALO) {
         if (TP == 10 - STAGES && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
       }
       if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
+      if constexpr (WIN) {
+        if (TP == 0 && !last_blk) issue_win(w_j + 1, (w_j + 1) & 1);
+      }
       if (RPF && rpf_loop && t == rpf_step) issue_res(lds + rpf_off);
     };
     if constexpr (MODE == (int)Prec::F16) {
@@ -1136,6 +1261,14 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       }
       issue_next();
       SPI_STAMP(st_c);
+      if constexpr (WIN) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const bool ok = tap_ok(i);
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[kk][i] = ok ? af[kk][i] : half8{};
+        }
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1167,6 +1300,14 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       }
       issue_next();
       SPI_STAMP(st_c);
+      if constexpr (WIN) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const bool ok = tap_ok(i);
+          ar0[i] = ok ? ar0[i] : u32x4{};
+          ar1[i] = ok ? ar1[i] : u32x4{};
+        }
+      }
       half8 ah[TI], al[TI];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
@@ -1274,6 +1415,19 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         kstep(t + 8, nx(), std::integral_constant<int, 8>{}, lb, Hs);
       }
     }
+  } else if constexpr (WIN) {
+    // one super-step (kh, channel block) per iteration, its three kw taps unrolled: the W
+    // stage is kw (slices start at a multiple of 3 steps), the window buffer j & 1
+    const int ns = nsteps / 3;
+    for (int j = 0; j < ns; ++j) {
+      const char* Ws = lds + STAGES * IMG + (j & 1) * HBUF;
+      w_tap0 = ((w_g0 + j) >> w_nbs) * 3;
+      w_j = j;
+      const bool lb = j == ns - 1;
+      kstep(3 * j, I0{}, I0{}, lb, Ws);
+      kstep(3 * j + 1, I1{}, I1{}, lb, Ws);
+      kstep(3 * j + 2, I2{}, I2{}, lb, Ws);
+    }
   } else if constexpr (TAP) {
     // unrolled by STAGES: stage offsets are immediates (the conv loop is short;
     // unrolling the large dense-GEMM bodies measured 1-2 % slower end to end)
@@ -1307,7 +1461,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 #endif
   if (!kSplitK<BM, BN, KIND> || a.splits == 1) {
     if (RPF && rpf_loop)
-      finish(acc, ((nsteps - 1) % STAGES) * IMG, lds + rpf_off);
+      finish(acc, park_off, lds + rpf_off);
     else
       finish(acc, 0, nullptr);
     tl_out(0);
@@ -1347,7 +1501,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     return;
   }
   const bool rpf_red = RPF && rpf_tile;
-  if (rpf_red) issue_res(lds + IMG);  // the parked tile takes [0, IMG)
+  if (rpf_red) issue_res(lds + (WIN ? STAGES * IMG : IMG));  // the parked tile takes [0, 16 KiB)
   if (tid == 0) {
     while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
       __builtin_amdgcn_s_sleep(1);
@@ -1412,6 +1566,7 @@ struct Plan {
   // period (rows per image) and offset (KArgs::h_off), band count, channel blocks
   // per slice
   int halo = 0, nw = 4, th = 0, period = 0, off = 0, tiles_m = 0, bps = 0;
+  int win = 0;  // kConvTapW (64 x 64, 3 W stages; slices of whole 3-step super-steps)
 };
 
 int estep_of(Prec prec) {
@@ -1437,6 +1592,7 @@ struct Knobs {
   int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
   int max_split = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
+  int win = 1;   // SPI_GEMM_WIN=0: 3x3/s1 tap walks without the kw window (kConvTapW)
   int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
   // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
   // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
@@ -1507,6 +1663,7 @@ Knobs read_knobs() {
     }
   }
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SPI_GEMM_WIN"); e && *e) k.win = std::atoi(e) != 0;
   return k;
 }
 
@@ -1581,6 +1738,16 @@ Plan halo_candidate(const GemmDesc& d, Prec prec, int T, int bm, bool stacked, i
   h.halo = small ? 2 : 1;
   h.bps = bps;
   return h;
+}
+
+// kConvTapW: 3x3 / stride 1 / padding 1 convs with OH = H, OW = W (a tap's input pixel is
+// the output pixel shifted by a constant), whole channel blocks, no Kpad tail, and A in
+// 128-byte pixel blocks read as they are (fp16, split fp16x3).
+bool window_ok(const GemmDesc& d, Prec prec) {
+  const int ES = estep_of(prec);
+  return knobs().win && d.conv && !d.pool_rows && d.KH == 3 && d.KW == 3 && d.stride == 1 && d.pad == 1 &&
+         d.OH == d.H && d.OW == d.W && d.krep == 1 && d.Cin >= ES && d.Cin % ES == 0 && d.Kpad == d.K &&
+         (prec == Prec::F16 || (prec == Prec::F16X3 && d.a_split));
 }
 
 Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
@@ -1660,7 +1827,14 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
   const int t64 = tiles_of(64, 64);
   const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
-  return finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
+  const Plan pl = finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
+  if (window_ok(d, prec)) {
+    // the kw-window tap walk: slices of whole (kh, channel block) super-steps
+    Plan w = finish_plan(Plan{64, 64, 3, sp, 0}, ksteps, ES, 3);
+    w.win = 1;
+    return w;
+  }
+  return pl;
 }
 
 int ilog2(int v) {
@@ -1730,6 +1904,7 @@ KArgs make_args(const GemmDesc& d, const GemmPtrs& p, const Plan& pl) {
     a.fd_period = make_fastdiv((unsigned)std::max(1, pl.period));
     a.fd_hwp = make_fastdiv((unsigned)a.h_hwp);
   }
+  if (pl.win) a.win_nblk_shift = ilog2(d.Cin / Traits<MODE>::ESTEP);
   return a;
 }
 
@@ -1748,6 +1923,11 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
       else
         SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvHalo>), grid, dim3(256), 0, s, g);
     }
+    return;
+  }
+  if (pl.win) {
+    if constexpr (MODE == (int)Prec::F16 || MODE == kF16X3S)
+      SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);
     return;
   }
   if (pl.bm == 128 && pl.bn == 128)
@@ -1833,7 +2013,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
     p1s.counters = p0.counters + 2 * g.a[0].tiles;
   }
   g.a[1] = make_args<MODE>(d1, p1s, q1);
-  const bool same = !q0.halo && !q1.halo && q0.bm == q1.bm && q0.bn == q1.bn &&
+  const bool same = !q0.halo && !q1.halo && !q0.win && !q1.win && q0.bm == q1.bm && q0.bn == q1.bn &&
                     q0.stages == q1.stages && q0.nw == 4 && q1.nw == 4 && g.a[0].cell_uniform &&
                     g.a[1].cell_uniform;
   if (!same) {
@@ -1871,6 +2051,34 @@ extern "C" void spi_debug_gemm_reload_env(void) {
   conv_wres_reload_env();
   gemm256_reload_env();
   attention_reload_env();
+}
+
+// The plan gemm() would pick for a conv (tests: which kind runs): out[0..7] = bm, bn, stages,
+// splits, halo kind, window kind, waves, k per slice.  precision as spi_ops.h (3 = split).
+extern "C" int spi_debug_conv_plan(int precision, int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                   int pad, int* out) {
+  if (!out || precision < 0 || precision > 3) return 1;
+  GemmDesc d;
+  d.conv = true;
+  d.H = H;
+  d.W = W;
+  d.Cin = Cin;
+  d.KH = KH;
+  d.KW = KW;
+  d.stride = stride;
+  d.pad = pad;
+  d.OH = (H + 2 * pad - KH) / stride + 1;
+  d.OW = (W + 2 * pad - KW) / stride + 1;
+  d.M = B * d.OH * d.OW;
+  d.N = Cout;
+  d.K = KH * KW * Cin;
+  d.Kpad = (d.K + 63) / 64 * 64;
+  d.a_split = d.out_split = precision == 3;
+  const Prec prec = precision == 0 ? Prec::F32 : precision == 1 ? Prec::F16 : Prec::F16X3;
+  const Plan pl = choose_plan(d, prec);
+  const int v[8] = {pl.bm, pl.bn, pl.stages, pl.splits, pl.halo, pl.win, pl.nw, pl.k_per_split};
+  for (int i = 0; i < 8; ++i) out[i] = v[i];
+  return 0;
 }
 
 #ifdef SPI_GEMM_STAMPS

@@ -161,6 +161,68 @@ def test_conv2d_split_layout(ops, B, H, cin, cout, k, stride, res):
     assert err < 1e-5, f"split conv {B}x{H}x{cin}->{cout} k{k}s{stride}: {err:.3e}"
 
 
+def conv_plan(ops, prec_id, B, H, cin, cout, k=3, stride=1, pad=1):
+    import ctypes as C
+    out = (C.c_int * 8)()
+    assert ops.lib.spi_debug_conv_plan(prec_id, B, H, H, cin, cout, k, k, stride, pad, out) == 0
+    return dict(zip(("bm", "bn", "stages", "splits", "halo", "win", "nw", "k_per_split"), list(out)))
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp16x3s"])
+@pytest.mark.parametrize("B,H,cin,cout,res", [(8, 28, 128, 128, True), (8, 14, 256, 256, True), (8, 7, 512, 512, False),
+                                              (3, 5, 64, 64, True), (2, 13, 128, 64, False), (1, 3, 64, 128, True),
+                                              (5, 9, 64, 64, True), (32, 7, 512, 512, True), (1, 28, 128, 128, False)])
+def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
+    """kConvTapW (round 4): the 3x3/s1 tap walk whose three kw taps share one DMA'd window of
+    66 consecutive pixels, taps in the padding zeroed at fragment read -- every 64x64 tap plan
+    of such a conv (split-K slices of whole (kh, channel block) super-steps; ragged M, maps 3 to
+    28 wide, several images per tile).  Checked against an fp32 conv and against the plain tap
+    walk (SPI_GEMM_WIN=0); halo kinds and the weight-resident 64->64 conv off so every shape
+    takes it."""
+    import os
+    g = torch.Generator().manual_seed(B * 7 + H * 3 + cin + cout)
+    x = torch.randn(B, H, H, cin, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g)
+    r = torch.randn(B, H, H, cout, generator=g) if res else None
+    split = prec == "fp16x3s"
+    if split:
+        xin, rin = ops.to_split(x), (ops.to_split(r) if res else None)
+        x_val = ops.from_split(xin)
+        r_val = ops.from_split(rin) if res else None
+        w_ref = w
+    else:
+        xin, rin = x.half(), (r.half() if res else None)
+        x_val, r_val, w_ref = xin.float(), (rin.float() if res else None), w.half().float()
+    ref = F.conv2d(x_val.permute(0, 3, 1, 2), w_ref, b, 1, 1).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + r_val
+    ref = F.relu(ref)
+    wp = ops.pack_weight(prec, ops.conv_weight_matrix(w, cin))
+    outs = {}
+    try:
+        os.environ["SPI_GEMM_HALO_CFG"] = "0"
+        os.environ["SPI_CONV_WRES"] = "0"
+        for win in ("1", "0"):
+            os.environ["SPI_GEMM_WIN"] = win
+            ops.lib.spi_debug_gemm_reload_env()
+            pl = conv_plan(ops, 3 if split else 1, B, H, cin, cout)
+            assert pl["win"] == int(win) and pl["bm"] == 64, pl
+            out = ops.conv2d(prec, xin.cuda(), wp, cout, 3, 3, 1, 1, bias=b.cuda(), act="relu",
+                             residual=rin.cuda() if res else None)
+            torch.cuda.synchronize()
+            outs[win] = (ops.from_split(out.cpu()) if split else out.float().cpu())
+    finally:
+        os.environ.pop("SPI_GEMM_HALO_CFG", None)
+        os.environ.pop("SPI_CONV_WRES", None)
+        os.environ.pop("SPI_GEMM_WIN", None)
+        ops.lib.spi_debug_gemm_reload_env()
+    tol = 1e-5 if split else 2e-3
+    for win, o in outs.items():
+        err = normalized_max_error(o.numpy(), ref.numpy())
+        assert err < tol, f"{prec} 3x3 conv B{B} H{H} {cin}->{cout} window={win}: {err:.3e}"
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 64, 64), (100, 96, 160), (392, 512, 4608), (1024, 768, 3072),
                                    (3152, 3072, 1024)])
 def test_gemm_split_layout(ops, M, N, K):
