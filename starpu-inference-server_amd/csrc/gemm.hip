@@ -338,15 +338,17 @@ constexpr bool kIsHalo = KIND == kConvHalo || KIND == kConvHaloS;
 // reading one A window.  For stride 1 and padding 1 (OH = H, OW = W) the input pixel of tap
 // (kh, kw) of output row m is the global pixel m + (kh - 1) W + kw - 1, so the 64 rows of a
 // tile read, for the three kw taps, the 66 consecutive pixels from m0 + (kh - 1) W - 1 on:
-// one DMA'd window of kWinRows rows (2 x 16-byte pieces + 1 x 4-byte piece per wave: 72
-// rows) feeds 3 k-steps -- 9 KiB of A per 3 steps instead of 24 (a tile step's LDS ingest
-// 16 -> 11 KiB; the layer-2..4 convs run at the per-CU ingest ceiling).
+// one DMA'd window of BM + 8 rows (BM / 32 16-byte pieces + one 4-byte piece per wave) feeds
+// 3 k-steps -- for 64-row tiles 9 KiB of A per 3 steps instead of 24 (a step's LDS ingest 16 ->
+// 11 KiB; 128-row tiles 24 -> 13.7 KiB; the tap walks run at the per-CU ingest ceiling,
+// DESIGN.md 3.1.5).
 // Taps that fall into the padding read a real neighbour pixel of the window and are zeroed
 // at fragment read by the row's tap mask.  Only W goes through the STAGES ring.
-constexpr int kWinRows = 72;
+template <int BM>
+constexpr int kWinRows = BM + 8;
 template <int BM, int BN, int STAGES, int KIND, int NW>
 constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND, NW> * NW * 8 * 128 + 16
-                          : KIND == kConvTapW ? STAGES * BN * 128 + 2 * kWinRows * 128 + 16
+                          : KIND == kConvTapW ? STAGES * BN * 128 + 2 * kWinRows<BM> * 128 + 16
                                               : STAGES * (BM + BN) * 128 + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
 // size per wave, capped by what the tile's LDS ring allows (NW / 4 waves per SIMD
@@ -368,7 +370,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   constexpr bool HALO = kIsHalo<KIND>;
   constexpr bool WIN = KIND == kConvTapW;
   constexpr bool AR = !HALO && !WIN;  // A tiles go through the ring
-  static_assert(!WIN || (BM == 64 && BN == 64 && NW == 4 && STAGES == 3), "window kind: 64 x 64, 4 waves, 3 W stages");
+  static_assert(!WIN || ((BM == 64 || BM == 128) && BN == 64 && NW == 4 && STAGES == 3),
+                "window kind: 64 / 128 x 64 tiles, 4 waves, 3 W stages");
   constexpr int NT = 64 * NW;  // threads per workgroup
   static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
   using TR = Traits<MODE>;
@@ -382,7 +385,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   static_assert(BQ * RPI * NW == BN, "W image rows per wave");
   constexpr int QPS = (AR ? AQ : 0) + BQ;
   constexpr int HQ = HALO ? kHaloHQ<BM, KIND, NW> : 1;  // halo DMA instructions per wave per block
-  constexpr int HBUF = HALO ? HQ * NW * RPI * RB : WIN ? kWinRows * RB : 0;  // bytes per halo / window buffer
+  constexpr int HBUF = HALO ? HQ * NW * RPI * RB : WIN ? kWinRows<BM> * RB : 0;  // bytes per halo / window buffer
+  constexpr int XQ = BM / 32 + 1;  // window kind: DMA pieces per wave per window
   constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND, NW>;
   static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
   static_assert(!WIN || RB == 128, "window rows are 128-byte pixel blocks");
@@ -611,23 +615,23 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   };
   // Window kind: super-step j of the slice is global super-step w_g0 + j = (kh, channel block
   // cb), kh-major (g = kh * nblk + cb); its k-step 3 j + kw reads W k-step (kh * 3 + kw) *
-  // nblk + cb (k = tap * Cin + c).  DMA side of a window: pieces 0, 1 of wave w (16 bytes a
-  // lane) fill rows 16 w + 8 q + lane / 8, slot lane & 7; piece 2 (4 bytes a lane) rows
-  // 64 + 2 w + lane / 32, slot (lane & 31) / 4 -- w_off: the source byte offset in the pixel's
-  // 128-byte block (chunk slot ^ (row & 7), the ring images' swizzle).
+  // nblk + cb (k = tap * Cin + c).  DMA side of a window: pieces q < BM / 32 of wave w (16
+  // bytes a lane) fill rows (BM / 4) w + 8 q + lane / 8, slot lane & 7; the last piece (4 bytes
+  // a lane) rows BM + 2 w + lane / 32, slot (lane & 31) / 4 -- w_off: the source byte offset in
+  // the pixel's 128-byte block (chunk slot ^ (row & 7), the ring images' swizzle).
   [[maybe_unused]] const int w_g0 = WIN ? kbeg / (3 * ESTEP) : 0;
   [[maybe_unused]] const int w_nbs = WIN ? a.win_nblk_shift : 0;
-  [[maybe_unused]] int w_row[3], w_off[3];
+  [[maybe_unused]] int w_row[XQ], w_off[XQ];
   if constexpr (WIN) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = wave * 16 + q * 8 + (lane >> 3);
+    for (int q = 0; q < XQ - 1; ++q) {
+      const int r = wave * (BM / 4) + q * 8 + (lane >> 3);
       w_row[q] = r;
       w_off[q] = ((lane & 7) ^ (r & 7)) << 4;
     }
-    const int r = 64 + wave * 2 + (lane >> 5);
-    w_row[2] = r;
-    w_off[2] = ((((lane & 31) >> 2) ^ (r & 7)) << 4) + ((lane & 3) << 2);
+    const int r = BM + wave * 2 + (lane >> 5);
+    w_row[XQ - 1] = r;
+    w_off[XQ - 1] = ((((lane & 31) >> 2) ^ (r & 7)) << 4) + ((lane & 3) << 2);
   }
   auto issue_win = [&](int jj, int buf) {
     if constexpr (WIN) {
@@ -637,13 +641,13 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       const char* base = reinterpret_cast<const char*>(Ap) + cb * RB;
       char* dst = lds + STAGES * IMG + buf * HBUF;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < XQ; ++q) {
         const int pix = p0 + w_row[q];
         const char* src = (unsigned)pix < (unsigned)d.M ? base + ((size_t)pix << (a.cin_shift + PSH)) + w_off[q] : zeros;
-        if (q < 2)
-          glds16(SPI_A_SRC(src), dst + (wave * 2 + q) * 1024);
+        if (q < XQ - 1)
+          glds16(SPI_A_SRC(src), dst + (wave * (XQ - 1) + q) * 1024);
         else
-          glds4(SPI_A_SRC(src), dst + 64 * RB + wave * 256);
+          glds4(SPI_A_SRC(src), dst + BM * RB + wave * 256);
       }
     }
   };
@@ -1174,7 +1178,6 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       // needs W(3j + 1) (W(3j + 2) and window j + 1 in flight), 3j + 2 needs W(3j + 2)
       // (window j + 1 and W(3j + 3)); last_blk: no super-step follows.  The residual
       // prefetch (issued at step 3j + 1 of the last super-step) stays in flight at 3j + 2.
-      constexpr int XQ = 3;  // window pieces per wave
       if constexpr (TP == 0) {
         dma_wait_barrier<BQ>();
       } else if constexpr (TP == 1) {
@@ -1501,7 +1504,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     return;
   }
   const bool rpf_red = RPF && rpf_tile;
-  if (rpf_red) issue_res(lds + (WIN ? STAGES * IMG : IMG));  // the parked tile takes [0, 16 KiB)
+  if (rpf_red) issue_res(lds + (WIN ? STAGES * IMG : IMG));  // the parked tile takes [0, BM * BN * 4)
   if (tid == 0) {
     while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
       __builtin_amdgcn_s_sleep(1);
@@ -1824,7 +1827,14 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   const int T = k.target;
   if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);
-  if (tiles_of(128, 64) >= T) return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
+  if (tiles_of(128, 64) >= T) {
+    if (window_ok(d, prec)) {
+      Plan w = finish_plan(Plan{128, 64, 3, 1, 0}, ksteps, ES, 3);
+      w.win = 1;
+      return w;
+    }
+    return finish_plan(Plan{128, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);
+  }
   const int t64 = tiles_of(64, 64);
   const int sp = t64 >= T ? 1 : std::max(1, std::min((T + t64 - 1) / t64, ksteps / 6));
   const Plan pl = finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
@@ -1926,8 +1936,12 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
     return;
   }
   if (pl.win) {
-    if constexpr (MODE == (int)Prec::F16 || MODE == kF16X3S)
-      SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);
+    if constexpr (MODE == (int)Prec::F16 || MODE == kF16X3S) {
+      if (pl.bm == 128)
+        SPI_LAUNCH((gemm_kernel<MODE, 128, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);
+      else
+        SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);
+    }
     return;
   }
   if (pl.bm == 128 && pl.bn == 128)

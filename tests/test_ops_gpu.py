@@ -171,11 +171,13 @@ def conv_plan(ops, prec_id, B, H, cin, cout, k=3, stride=1, pad=1):
 @pytest.mark.parametrize("prec", ["fp16", "fp16x3s"])
 @pytest.mark.parametrize("B,H,cin,cout,res", [(8, 28, 128, 128, True), (8, 14, 256, 256, True), (8, 7, 512, 512, False),
                                               (3, 5, 64, 64, True), (2, 13, 128, 64, False), (1, 3, 64, 128, True),
-                                              (5, 9, 64, 64, True), (32, 7, 512, 512, True), (1, 28, 128, 128, False)])
+                                              (5, 9, 64, 64, True), (32, 7, 512, 512, True), (1, 28, 128, 128, False),
+                                              # 128 x 64 tiles (136-row windows)
+                                              (32, 14, 256, 256, True), (16, 28, 128, 128, False)])
 def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
     """kConvTapW (round 4): the 3x3/s1 tap walk whose three kw taps share one DMA'd window of
-    66 consecutive pixels, taps in the padding zeroed at fragment read -- every 64x64 tap plan
-    of such a conv (split-K slices of whole (kh, channel block) super-steps; ragged M, maps 3 to
+    BM + 2 consecutive pixels, taps in the padding zeroed at fragment read -- every 64x64 and
+    128x64 tap plan of such a conv (split-K slices of whole (kh, channel block) super-steps; ragged M, maps 3 to
     28 wide, several images per tile).  Checked against an fp32 conv and against the plain tap
     walk (SPI_GEMM_WIN=0); halo kinds and the weight-resident 64->64 conv off so every shape
     takes it."""
@@ -207,7 +209,9 @@ def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
             os.environ["SPI_GEMM_WIN"] = win
             ops.lib.spi_debug_gemm_reload_env()
             pl = conv_plan(ops, 3 if split else 1, B, H, cin, cout)
-            assert pl["win"] == int(win) and pl["bm"] == 64, pl
+            assert pl["win"] == int(win) and pl["bm"] in (64, 128), pl
+            if win == "1":
+                assert pl["bm"] == (128 if B * H * H >= 6272 else 64), pl
             out = ops.conv2d(prec, xin.cuda(), wp, cout, 3, 3, 1, 1, bias=b.cuda(), act="relu",
                              residual=rin.cuda() if res else None)
             torch.cuda.synchronize()
