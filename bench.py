@@ -330,8 +330,6 @@ def runtime_e2e(rtmod, replica, name, batch, requests, inflight, req_batch=None,
     rt = rtmod.Runtime([replica], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=workers,
                        **kw)
     h2d = rt.h2d_mode
-    if rt.h2d_wait:
-        h2d += f" ({rt.h2d_wait} wait)"
     r = rt.loadgen(host_inputs, requests=requests, inflight=inflight,
                    warmup=warmup if warmup is not None else max(8 * workers, 2 * inflight), schedule=schedule)
     target = rt.batch_target

@@ -207,10 +207,6 @@ int32_t spi_runtime_num_workers(const spi_runtime* rt);
 int spi_runtime_worker_times(const spi_runtime* rt, int32_t worker, int64_t* out);
 /* The H2D mode the runtime resolved (SPI_H2D_AUTO -> one of the concrete modes). */
 int32_t spi_runtime_h2d_mode(const spi_runtime* rt);
-/* SPI_H2D_WORKER_SDMA only: 1 when the worker streams wait for the SDMA copies on the device
- * (hipStreamWaitValue64 on the slot signal), 0 when the worker threads wait on the host
- * (SPI_H2D_SDMA_WAIT=host, or the device refused the stream wait); -1 in the other modes. */
-int32_t spi_runtime_h2d_device_wait(const spi_runtime* rt);
 /* Current adaptive target batch limit (samples); the fixed limit otherwise. */
 int32_t spi_runtime_batch_target(const spi_runtime* rt);
 /* Wall time spi_runtime_create spent in the per-worker warm-up (graph captures, workspaces). */

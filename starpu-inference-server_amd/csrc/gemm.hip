@@ -1504,7 +1504,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     return;
   }
   const bool rpf_red = RPF && rpf_tile;
-  if (rpf_red) issue_res(lds + (WIN ? STAGES * IMG : IMG));  // the parked tile takes [0, BM * BN * 4)
+  char* const red_res = lds + (WIN ? STAGES * IMG : IMG);  // the parked tile takes [0, BM * BN * 4)
+  if (rpf_red) issue_res(red_res);
   if (tid == 0) {
     while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
       __builtin_amdgcn_s_sleep(1);
@@ -1542,7 +1543,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         for (int j = 0; j < TJ; ++j) sum[i][j] += own ? acc[i][j] : v[zz][i][j];
     }
   }
-  finish(sum, 0, rpf_red ? lds + IMG : nullptr);
+  finish(sum, 0, rpf_red ? red_res : nullptr);
   tl_out(2);
   }
 }

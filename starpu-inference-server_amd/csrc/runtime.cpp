@@ -209,10 +209,8 @@ struct Job {
 struct Slot {
   std::vector<void*> h_in, h_out, d_in, d_out;
   hipEvent_t h2d = nullptr, done = nullptr;
-  // SPI_H2D_WORKER_SDMA: completion signal of this slot's SDMA copies (value = copies in
-  // flight) and its value word, which the worker stream waits on (hipStreamWaitValue64)
+  // SPI_H2D_WORKER_SDMA: completion signal of this slot's SDMA copies (value = copies in flight)
   hsa_signal_t sig{};
-  volatile hsa_signal_value_t* sig_val = nullptr;
 };
 
 // SlotPoolBase::acquire / try_acquire / release (slot_pool_base.hpp:32-75).
@@ -256,7 +254,6 @@ struct Task {
   int status = SPI_OK;
   std::string err;
   int64_t cs = 0, ce = 0;
-  bool sdma_pending = false;  // its SDMA copies were waited on the device only
 };
 
 struct Worker {
@@ -377,12 +374,6 @@ struct spi_runtime {
   std::vector<std::unique_ptr<SlotPool>> pools;
   std::vector<std::unique_ptr<Worker>> workers;
   std::unique_ptr<CopyPool> copier;
-  // SPI_H2D_WORKER_SDMA: the worker STREAM waits for the copies (hipStreamWaitValue64 on the
-  // slot signal's value word) and the thread moves on -- StarPU orders a task's transfers
-  // before its codelet without blocking the submitter (slot_manager_component.cpp:222-293).
-  // False when the device cannot (checked at create) or SPI_H2D_SDMA_WAIT=host: the worker
-  // thread waits on the signal before enqueueing the codelet (round 3).
-  bool sdma_stream_wait = false;
   // SPI_RT_COMPLETION=spin: finalize polls the completion event (yielding) instead of
   // hipEventSynchronize (read at create)
   bool spin_completion = false;
@@ -516,30 +507,17 @@ void spi_runtime::launch(Worker* w, std::vector<Job>&& jobs) {
         hsa_signal_subtract_screlease(slot.sig, ni - i);
         break;
       }
-    if (sdma_stream_wait) {
-      // the codelet runs behind the copies on the device; finalize_oldest checks the signal
-      if (hipStreamWaitValue64(w->stream, (void*)slot.sig_val, 0, hipStreamWaitValueEq, ~0ull) != hipSuccess) {
-        hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
-        while (v >= 1) v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                                     HSA_WAIT_STATE_ACTIVE);
-        if (v < 0 && t.status == SPI_OK) {
-          t.status = SPI_ERR_DEVICE;
-          t.err = "SDMA H2D failed";
-        }
-      } else {
-        t.sdma_pending = true;
-      }
-    } else {
-      // A wait may return before the condition holds (the HSA spec allows it;
-      // ROCclr loops too): wait until the value drops below 1.  Each completed copy
-      // decrements it; a failed copy leaves it negative.
-      hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
-      while (v >= 1)
-        v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
-      if (v < 0 && t.status == SPI_OK) {
-        t.status = SPI_ERR_DEVICE;
-        t.err = "SDMA H2D failed";
-      }
+    // The worker thread waits (round 4 measured the alternative -- the worker stream waiting on
+    // the signal's value word with hipStreamWaitValue64 -- releasing 46-55 ms after the copy on
+    // this stack, tools/sdma_streamwait.cpp).  A wait may return before the
+    // condition holds (the HSA spec allows it; ROCclr loops too): wait until the value drops
+    // below 1.  Each completed copy decrements it; a failed copy leaves it negative.
+    hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
+    while (v >= 1)
+      v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    if (v < 0 && t.status == SPI_OK) {
+      t.status = SPI_ERR_DEVICE;
+      t.err = "SDMA H2D failed";
     }
   }
   for (int i = 0; i < ni && t.status == SPI_OK && cfg.h2d_mode != SPI_H2D_WORKER_SDMA; ++i)
@@ -629,20 +607,6 @@ void spi_runtime::finalize_oldest(Worker* w) {
   SlotPool& pool = *pools[w->pool];
   Slot& slot = pool.slots[t.slot];
   const int64_t e0 = now_ns();
-  if (t.sdma_pending) {
-    // the stream waits for this slot's signal to reach 0; a failed copy leaves it negative:
-    // fail the task and release the stream (it runs the codelet on stale inputs, reported failed)
-    hsa_signal_value_t v = hsa_signal_load_scacquire(slot.sig);
-    while (v >= 1)
-      v = hsa_signal_wait_scacquire(slot.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
-    if (v < 0) {
-      hsa_signal_store_screlease(slot.sig, 0);
-      if (t.status == SPI_OK) {
-        t.status = SPI_ERR_DEVICE;
-        t.err = "SDMA H2D failed";
-      }
-    }
-  }
   hipError_t se;
   if (spin_completion) {
     while ((se = hipEventQuery(slot.done)) == hipErrorNotReady) std::this_thread::yield();
@@ -927,8 +891,7 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     }
     if (ok && cfg.h2d_mode == SPI_H2D_WORKER_SDMA)
       for (Slot& sl : pool->slots)
-        ok = ok && hsa_signal_create(0, 0, nullptr, &sl.sig) == HSA_STATUS_SUCCESS &&
-             hsa_amd_signal_value_pointer(sl.sig, &sl.sig_val) == HSA_STATUS_SUCCESS;
+        ok = ok && hsa_signal_create(0, 0, nullptr, &sl.sig) == HSA_STATUS_SUCCESS;
     rt->pools.push_back(std::move(pool));
     if (!ok) return cleanup_fail("slot pool allocation failed on device " + std::to_string(c->device_ids[dv]));
     for (int k = 0; k < cfg.workers_per_device; ++k) {
@@ -1007,23 +970,6 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   }
   rt->warmup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - warm_t0).count();
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
-  if (cfg.h2d_mode == SPI_H2D_WORKER_SDMA) {
-    // the worker streams wait for the copies unless SPI_H2D_SDMA_WAIT=host (A/B) or the device
-    // refuses the wait: one on an already-satisfied value word per worker stream first
-    const char* e = std::getenv("SPI_H2D_SDMA_WAIT");
-    rt->sdma_stream_wait = !(e && std::strcmp(e, "host") == 0);
-    for (auto& w : rt->workers) {
-      if (!rt->sdma_stream_wait) break;
-      (void)hipSetDevice(w->device);
-      Slot& sl = rt->pools[w->pool]->slots[0];
-      hsa_signal_store_screlease(sl.sig, 0);
-      if (hipStreamWaitValue64(w->stream, (void*)sl.sig_val, 0, hipStreamWaitValueEq, ~0ull) != hipSuccess ||
-          hipStreamSynchronize(w->stream) != hipSuccess) {
-        (void)hipGetLastError();
-        rt->sdma_stream_wait = false;
-      }
-    }
-  }
   if (const char* e = std::getenv("SPI_RT_COMPLETION"); e && std::strcmp(e, "spin") == 0) rt->spin_completion = true;
   rt->last_target = cfg.max_batch;
   for (auto& w : rt->workers) w->thread = std::thread(&spi_runtime::run, rt.get(), w.get());
@@ -1110,10 +1056,7 @@ int32_t spi_runtime_h2d_mode(const spi_runtime* rt) { return rt ? rt->cfg.h2d_mo
 
 double spi_runtime_warmup_seconds(const spi_runtime* rt) { return rt ? rt->warmup_s : 0.0; }
 
-int32_t spi_runtime_h2d_device_wait(const spi_runtime* rt) {
-  if (!rt || rt->cfg.h2d_mode != SPI_H2D_WORKER_SDMA) return -1;
-  return rt->sdma_stream_wait ? 1 : 0;
-}
+
 
 int32_t spi_runtime_batch_target(const spi_runtime* rt) {
   if (!rt) return 0;

@@ -117,7 +117,6 @@ for _name, _res, _args in [
     ("spi_runtime_batch_target", C.c_int32, [C.c_void_p]),
     ("spi_runtime_warmup_seconds", C.c_double, [C.c_void_p]),
     ("spi_runtime_h2d_mode", C.c_int32, [C.c_void_p]),
-    ("spi_runtime_h2d_device_wait", C.c_int32, [C.c_void_p]),
     ("spi_runtime_destroy", None, [C.c_void_p]),
     ("spi_runtime_loadgen", C.c_int, [C.c_void_p, C.POINTER(LoadgenConfig), C.POINTER(C.c_void_p),
                                       C.POINTER(LoadgenResult)]),
@@ -247,13 +246,6 @@ class Runtime:
         """The H2D mode in effect (SPI_H2D_AUTO resolved at create)."""
         v = lib.spi_runtime_h2d_mode(self.handle)
         return next(k for k, m in H2D_MODES.items() if m == v)
-
-    @property
-    def h2d_wait(self):
-        """Who waits for an SDMA H2D copy: "stream" (the worker stream, on the device) or "host"
-        (the worker thread); None outside SPI_H2D_WORKER_SDMA."""
-        v = lib.spi_runtime_h2d_device_wait(self.handle)
-        return None if v < 0 else ("stream" if v else "host")
 
     @property
     def batch_target(self) -> int:

@@ -211,7 +211,8 @@ def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
             pl = conv_plan(ops, 3 if split else 1, B, H, cin, cout)
             assert pl["win"] == int(win) and pl["bm"] in (64, 128), pl
             if win == "1":
-                assert pl["bm"] == (128 if B * H * H >= 6272 else 64), pl
+                tiles128 = -(-B * H * H // 128) * -(-cout // 64)  # 128 x 64 tiles (plan target 128)
+                assert pl["bm"] == (128 if tiles128 >= 128 else 64), pl
             out = ops.conv2d(prec, xin.cuda(), wp, cout, 3, 3, 1, 1, bias=b.cuda(), act="relu",
                              residual=rin.cuda() if res else None)
             torch.cuda.synchronize()

@@ -195,25 +195,15 @@ def test_runtime_single_process_multi_device_adaptive(spi, zoo, rtmod):
     rt.close()
 
 
-@pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy", "worker_sdma",
-                                      "worker_sdma_host_wait"])
-def test_runtime_pipeline_with_small_slot_pool(spi, zoo, rtmod, h2d_mode, monkeypatch):
+@pytest.mark.parametrize("h2d_mode", ["device_stream", "worker_stream", "worker_copy", "worker_sdma"])
+def test_runtime_pipeline_with_small_slot_pool(spi, zoo, rtmod, h2d_mode):
     """Pipeline depth 3 per worker over a 2-slot pool (fewer slots than workers x depth): the
     worker must finalize its own finished tasks to free slots (SlotPoolBase::try_acquire /
-    acquire / release) -- every ragged job still matches its own forward.  worker_sdma: the
-    worker stream waits for the slot's SDMA signal on the device (round 4), so a slot is
-    restaged only after the codelet that read it finished; _host_wait: SPI_H2D_SDMA_WAIT=host."""
-    wait = None
-    if h2d_mode.startswith("worker_sdma"):
-        wait = "host" if h2d_mode.endswith("host_wait") else "stream"
-        h2d_mode = "worker_sdma"
-        if wait == "host":
-            monkeypatch.setenv("SPI_H2D_SDMA_WAIT", "host")
+    acquire / release) -- every ragged job still matches its own forward."""
     m = zoo.resnet18(image=64)
     rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=4, image_size=64)
     rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=4, workers_per_device=2,
                        pipeline_depth=3, slots_per_device=2, h2d_mode=h2d_mode, copy_threads=3)
-    assert rt.h2d_wait == wait
     rng = np.random.default_rng(8)
     jobs = []
     for rid in range(40):

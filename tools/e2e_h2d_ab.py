@@ -31,8 +31,7 @@ def main():
     rep = spi.ModelReplica(zoo.build(args.model, seed=0), 0, args.precision, max_batch=args.batch, graphs=True)
     for r in range(args.rounds):
         for spec in args.modes.split(","):
-            mode, _, wait = spec.partition(":")  # "worker_sdma:blocked" sleeps on the copy signal
-            os.environ["SPI_H2D_SDMA_WAIT"] = wait
+            mode = spec
             for inflight in (32, 16):
                 out = bench.runtime_e2e(rtmod, rep, args.model, args.batch, args.requests, inflight, h2d_mode=mode)
                 print(json.dumps({"round": r, "h2d_mode": spec, "inflight": inflight, **out}), flush=True)

@@ -1,5 +1,5 @@
 """Where the e2e tail comes from: the bench's e2e leg (ResNet-18 fp16m bs8, 4 workers, 32 in
-flight) repeated under runtime knobs read at create (SPI_RT_COMPLETION, SPI_H2D_SDMA_WAIT),
+flight) repeated under the runtime knob read at create (SPI_RT_COMPLETION),
 interleaved rounds in one process; prints one JSON line per run with the latency breakdown."""
 import importlib
 import json
@@ -16,12 +16,11 @@ zoo = importlib.import_module("starpu-inference-server_amd.zoo")
 rtmod = importlib.import_module("starpu-inference-server_amd.runtime")
 m = zoo.resnet18()
 rep = spi.ModelReplica(m, 0, "fp16m", max_batch=8, graphs=True)
-variants = [{}, {"SPI_RT_COMPLETION": "spin"}, {"SPI_H2D_SDMA_WAIT": "blocked"},
-            {"SPI_RT_COMPLETION": "spin", "SPI_H2D_SDMA_WAIT": "blocked"}]
+variants = [{}, {"SPI_RT_COMPLETION": "spin"}]
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 for rnd in range(rounds):
     for v in variants:
-        for k in ("SPI_RT_COMPLETION", "SPI_H2D_SDMA_WAIT"):
+        for k in ("SPI_RT_COMPLETION",):
             os.environ.pop(k, None)
         os.environ.update(v)
         for inflight in (32, 16):

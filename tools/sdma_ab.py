@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
-"""H2D A/B through the mini-runtime, interleaved rounds in one process: SDMA copies waited by the
-worker stream on the device (round 4 default), SDMA waited by the worker thread
-(SPI_H2D_SDMA_WAIT=host, round 3), and the worker-stream hipMemcpyAsync copies.  Each line: e2e
+"""H2D A/B through the mini-runtime, interleaved rounds in one process: SDMA copies (waited by the
+worker thread) against the worker-stream hipMemcpyAsync copies.  Each line: e2e
 rate, p50, and where the worker threads spent their time (spi_runtime_worker_times: slot wait,
 host staging, H2D + codelet + D2H enqueue, completion-event wait).
 
@@ -36,20 +35,14 @@ else:
 out_elems = int(np.prod(out_shape[1:]))
 requests = int(os.environ.get("REQUESTS", "400"))
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
-    for label, mode, wait in (("sdma/stream-wait", "worker_sdma", ""), ("sdma/host-wait", "worker_sdma", "host"),
-                              ("worker_stream", "worker_stream", "")):
-        os.environ.pop("SPI_H2D_SDMA_WAIT", None)
-        if wait:
-            os.environ["SPI_H2D_SDMA_WAIT"] = wait
+    for label, mode in (("worker_sdma", "worker_sdma"), ("worker_stream", "worker_stream")):
         rt = rtmod.Runtime([rep], in_specs, [(out_elems, np.float32)], max_batch=batch, workers_per_device=4,
                            h2d_mode=mode, warmup_batches=-1)
-        got_wait = rt.h2d_wait
         r = rt.loadgen(x, requests=requests, inflight=16, warmup=32)
         wt = rt.worker_times()
         rt.close()
         tot = {k: round(sum(w[k] for w in wt), 3) for k in ("slot_s", "stage_s", "enqueue_s", "event_s")}
-        print(json.dumps({"model": name, "round": rnd, "mode": label, "wait_in_effect": got_wait,
+        print(json.dumps({"model": name, "round": rnd, "mode": label,
                           "value": round(r["inferences_per_s"], 1), "p50": round(r["p50_ms"], 2),
                           "p99": round(r["p99_ms"], 2), "seconds": round(r["seconds"], 3),
                           "tasks": sum(w["tasks"] for w in wt), "worker_s": tot}), flush=True)
-os.environ.pop("SPI_H2D_SDMA_WAIT", None)

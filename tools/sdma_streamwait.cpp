@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -27,7 +28,7 @@ struct Agents {
   bool have_gpu = false, have_cpu = false;
 };
 
-int main() {
+int main(int argc, char** argv) {
   int can = 0;
   (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, 0);
   std::printf("CanUseStreamWaitValue=%d\n", can);
@@ -62,11 +63,16 @@ int main() {
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   (void)hipDeviceSynchronize();
 
+  // hsa_amd_signal_value_pointer needs an HSA_AMD_SIGNAL_AMD_GPU_ONLY or _IPC signal (a plain
+  // hsa_signal_create one returns INVALID_ARGUMENT): argv[1] = attribute bits (default 1)
+  const uint64_t attr = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 1;
   hsa_signal_t sig;
-  hsa_signal_create(1, 0, nullptr, &sig);
+  const hsa_status_t cs0 = hsa_amd_signal_create(1, 0, nullptr, attr, &sig);
   volatile hsa_signal_value_t* vp = nullptr;
   const hsa_status_t ps = hsa_amd_signal_value_pointer(sig, &vp);
-  std::printf("signal_value_pointer status=%d ptr=%p\n", (int)ps, (void*)vp);
+  std::printf("attributes=%llu create status=%d signal_value_pointer status=%d ptr=%p\n", (unsigned long long)attr,
+              (int)cs0, (int)ps, (void*)vp);
+  if (ps != HSA_STATUS_SUCCESS) return 0;  // not usable: reported above
   const hipError_t we = hipStreamWaitValue64(s, (void*)vp, 0, hipStreamWaitValueEq, ~0ull);
   std::printf("hipStreamWaitValue64 -> %s\n", hipGetErrorString(we));
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, s, d, n, flag);
