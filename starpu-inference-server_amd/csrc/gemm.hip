@@ -346,10 +346,14 @@ constexpr bool kIsHalo = KIND == kConvHalo || KIND == kConvHaloS;
 // at fragment read by the row's tap mask.  Only W goes through the STAGES ring.
 template <int BM>
 constexpr int kWinRows = BM + 8;
+// Dense kinds keep 2 x BM {mean, rstd} pairs past the ring for the LayerNorm fold (the tile's
+// row statistics, computed once per row before the epilogue's walk).
+template <int BM, int KIND>
+constexpr int kLnBytes = KIND == kDense ? 2 * BM * 8 : 0;
 template <int BM, int BN, int STAGES, int KIND, int NW>
 constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND, NW> * NW * 8 * 128 + 16
                           : KIND == kConvTapW ? STAGES * BN * 128 + 2 * kWinRows<BM> * 128 + 16
-                                              : STAGES * (BM + BN) * 128 + 16;
+                                              : STAGES * (BM + BN) * 128 + kLnBytes<BM, KIND> + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
 // size per wave, capped by what the tile's LDS ring allows (NW / 4 waves per SIMD
 // per block, 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
@@ -388,7 +392,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   constexpr int HBUF = HALO ? HQ * NW * RPI * RB : WIN ? kWinRows<BM> * RB : 0;  // bytes per halo / window buffer
   constexpr int XQ = BM / 32 + 1;  // window kind: DMA pieces per wave per window
   constexpr int LDSB = kLdsBytes<BM, BN, STAGES, KIND, NW>;
-  static_assert(LDSB == STAGES * IMG + 2 * HBUF + 16, "LDS layout");
+  static_assert(LDSB == STAGES * IMG + 2 * HBUF + kLnBytes<BM, KIND> + 16, "LDS layout");
   static_assert(!WIN || RB == 128, "window rows are 128-byte pixel blocks");
   static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -856,6 +860,15 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       bv0 = *reinterpret_cast<const floatx4*>(a.p.bias + nb_);
       bv1 = *reinterpret_cast<const floatx4*>(a.p.bias + nb_ + 4);
     }
+    // LayerNorm fold: the tile rows' {mean, rstd} once per row into LDS past the ring ([0, BM):
+    // the A rows' (consumer), [BM, 2 BM): the residual rows' (res_ln)); read after the park's barrier
+    [[maybe_unused]] float2* const ln_s = reinterpret_cast<float2*>(lds + STAGES * IMG + 2 * HBUF);
+    if constexpr (LNF) {
+      if (d.ln_in_chunks > 0)
+        ln_tile_stats(a.p.ln.in_stats, m0, BM, d.M, d.ln_in_chunks, d.ln_in_eps, ln_s, tid, NT);
+      if (d.res_ln_chunks > 0)
+        ln_tile_stats(a.p.ln.res_stats, m0, BM, d.M, d.res_ln_chunks, d.res_ln_eps, ln_s + BM, tid, NT);
+    }
     __syncthreads();  // every wave is done reading the ring
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -1042,11 +1055,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           if (d.res_ln_chunks > 0) {
 #pragma unroll
             for (int it = 0; it < CH; ++it) {
-              const int mr = row_m(r0 + (c0 + it) * RSTEP);
-              float mean, rstd;
-              ln_row_stats(a.p.ln.res_stats, mr < 0 ? 0 : mr, d.res_ln_chunks, d.res_ln_eps, mean, rstd);
+              const float2 st = ln_s[BM + r0 + (c0 + it) * RSTEP];
 #pragma unroll
-              for (int e = 0; e < 8; ++e) y[it][e] = (y[it][e] - mean) * rstd * lng[e] + lnb[e];
+              for (int e = 0; e < 8; ++e) y[it][e] = (y[it][e] - st.x) * st.y * lng[e] + lnb[e];
             }
           }
         }
@@ -1056,11 +1067,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           tile_vals(r0 + (c0 + it) * RSTEP, t);
           if constexpr (LNF) {
             if (d.ln_in_chunks > 0) {  // consumer: y = rstd (acc - mean c1) + bias
-              const int mr = row_m(r0 + (c0 + it) * RSTEP);
-              float mean, rstd;
-              ln_row_stats(a.p.ln.in_stats, mr < 0 ? 0 : mr, d.ln_in_chunks, d.ln_in_eps, mean, rstd);
+              const float2 st = ln_s[r0 + (c0 + it) * RSTEP];
 #pragma unroll
-              for (int e = 0; e < 8; ++e) t[e] = rstd * (t[e] - mean * lnc1[e]);
+              for (int e = 0; e < 8; ++e) t[e] = st.y * (t[e] - st.x * lnc1[e]);
             }
           }
 #pragma unroll

@@ -10,9 +10,29 @@
 namespace spi {
 
 // mean and rstd of row m from its `chunks` (mean, M2) partials over 64 columns each (Chan).
+// Up to 16 chunks (D <= 1024: every BERT / ViT width) all loads go out before any use -- one
+// memory latency per row; a loop of dependent loads per row had doubled the consuming GEMMs
+// (round 4, tools/loaded_ops.py).  Callers compute a tile's rows once, into LDS (ln_tile_stats).
 __device__ __forceinline__ void ln_row_stats(const float* stats, int m, int chunks, float eps, float& mean,
                                              float& rstd) {
   const float2* p = reinterpret_cast<const float2*>(stats) + (size_t)m * chunks;
+  if (chunks <= 16) {
+    float2 v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = c < chunks ? p[c] : float2{0.f, 0.f};
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s += v[c].x;
+    mean = s / (float)chunks;
+    float m2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float dm = v[c].x - mean;
+      m2 += c < chunks ? v[c].y + 64.f * dm * dm : 0.f;
+    }
+    rstd = rsqrtf(m2 / (64.f * (float)chunks) + eps);
+    return;
+  }
   float s = 0.f;
   for (int c = 0; c < chunks; ++c) s += p[c].x;
   mean = s / (float)chunks;
@@ -23,6 +43,16 @@ __device__ __forceinline__ void ln_row_stats(const float* stats, int m, int chun
     m2 += v.y + 64.f * dm * dm;
   }
   rstd = rsqrtf(m2 / (64.f * (float)chunks) + eps);
+}
+
+// {mean, rstd} of a tile's `rows` rows (m0 on, clamped to M - 1) into `out`, one row per thread.
+__device__ __forceinline__ void ln_tile_stats(const float* stats, int m0, int rows, int M, int chunks, float eps,
+                                              float2* out, int tid, int nthreads) {
+  for (int r = tid; r < rows; r += nthreads) {
+    float mean, rstd;
+    ln_row_stats(stats, min(m0 + r, M - 1), chunks, eps, mean, rstd);
+    out[r] = float2{mean, rstd};
+  }
 }
 
 // (mean, M2) of one row's 64-column chunk held as 8 values by each of 8 consecutive lanes

@@ -135,9 +135,9 @@ void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const
 // gemm() routes a desc to it when gemm256_eligible (N % 256 == 0, K % 64 == 0,
 // at least min_tiles 256^2 tiles; SPI_GEMM_256_MIN, default 128, 0 = never).
 bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
-// Split-K slices for a gemm256 problem: 1 with >= target tiles, else enough slices of >= 8
+// Split-K slices for a gemm256 problem: 1 with >= target tiles, else enough slices of >= 16
 // k-tiles (at most 4, at most max_split when > 0) to reach ~target workgroups (ViT-L's
-// N = 1024 GEMMs: 52 tiles -> FFN2 3 slices, out-proj 2).
+// N = 1024 GEMMs: 52 tiles -> FFN2 3 slices, out-proj none).
 int gemm256_splits(const GemmDesc& d, int target, int max_split);
 void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s);
 void gemm256_reload_env();  // no knobs left (kept for spi_debug_gemm_reload_env)

@@ -422,12 +422,13 @@ def test_gemm256_in_place_residual(ops, gemm256_everywhere, router, M, N, K):
 
 
 @pytest.mark.parametrize("maxsplit", ["1", "2", "3", "0"])
-@pytest.mark.parametrize("M,N,K,res", [(600, 512, 2048, "f32"), (3152, 1024, 1024, None), (257, 256, 1536, "f16")])
+@pytest.mark.parametrize("M,N,K,res", [(600, 512, 4096, "f32"), (3152, 1024, 2048, None), (257, 256, 3072, "f16")])
 def test_gemm256_split_k(ops, gemm256_everywhere, maxsplit, M, N, K, res):
-    """gemm256's split-K (grids under 128 workgroups: slices of >= 8 k-tiles, at most 4; the
+    """gemm256's split-K (grids under 128 workgroups: slices of >= 16 k-tiles, at most 4; the
     last slice to arrive sums the write-through slabs in slice order).  SPI_GEMM_MAXSPLIT caps
-    the slices (0 = uncapped: 4 for 600x512x2048, slices of 8 k-tiles; 3 gives a short last
-    slice).  The sum order does not depend on arrival: two launches agree bit for bit."""
+    the slices (0 = uncapped: 4 for 600x512x4096, 2 for 3152x1024x2048, 3 for 257x256x3072;
+    a cap of 3 on the first gives a short last slice).  The sum order does not depend on
+    arrival: two launches agree bit for bit."""
     import os
     os.environ["SPI_GEMM_MAXSPLIT"] = maxsplit
     ops.lib.spi_debug_gemm_reload_env()
