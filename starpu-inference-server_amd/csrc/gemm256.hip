@@ -120,9 +120,12 @@ __device__ __forceinline__ void bar() {
 // Ping-pong wave rows (the lock-step two-tile-ahead variant measured C5 -2.3 % and was removed, round 4)
 template <int RES>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
-  __shared__ int s_ticket;
-  __shared__ float2 ln_s[256];  // LayerNorm fold: the tile rows' {mean, rstd} (consumer)
+  // ONE LDS object: with a second __shared__ variable beside the k-tile buffers hipcc's waitcnt
+  // pass could no longer tell the LDS-DMA destinations from the fragment reads and put a
+  // vmcnt(0) in front of every phase's reads (ViT-L FFN1 / QKV +15 %, round 4)
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes + 256 * 8 + 16];
+  float2* const ln_s = reinterpret_cast<float2*>(lds + 2 * kBufBytes);  // LayerNorm fold: tile rows' {mean, rstd}
+  int* const s_ticket = reinterpret_cast<int*>(lds + 2 * kBufBytes + 256 * 8);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
@@ -276,9 +279,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     float* slabs = g.partial + (size_t)tile * g.splits * SLAB;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(slabs, (short)0, g.splits * SLAB * 4, 0x00020000);
-    if (tid == 0) s_ticket = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) *s_ticket = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (s_ticket < g.splits - 1) {
+    if (*s_ticket < g.splits - 1) {
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
