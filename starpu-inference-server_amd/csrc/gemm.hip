@@ -1160,9 +1160,14 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // the fragment reads -- is an immediate.
   // Halo steps also take the tap (a constant), whether this is the slice's last
   // channel block, and that block's halo buffer.
-  auto kstep = [&](int t, auto u_arg, auto tap_arg, bool last_blk, const char* Hs) {
+  // steady_c (std::true_type): a step that issues step t + STAGES - 1, waits for the full ring
+  // and is not at or after the residual prefetch -- no per-step checks at all (the loops below
+  // run every step that far from the slice's end this way; round 4 had them checked per step,
+  // ~55 SALU + 7 branches per step that made the ingest-bound loops 30 % slower)
+  auto kstep = [&](int t, auto u_arg, auto tap_arg, bool last_blk, const char* Hs, auto steady_c) {
     const int U = u_arg;  // a constant when u_arg is a std::integral_constant
     constexpr int TP = decltype(tap_arg)::value;
+    constexpr bool STEADY = decltype(steady_c)::value;
     SPI_STAMP(st_a);
     // Step t has landed once at most (issued steps after t) DMA groups remain.
     // Halo: W step t + 1 is in flight, and at tap 8 of a block that has a
@@ -1202,6 +1207,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
         else
           dma_wait_barrier<0>();
       }
+    } else if constexpr (STEADY) {
+      dma_wait_barrier<(STAGES - 2) * QPS>();
     } else {
       // steps after the residual prefetch (rpf_loop, issued youngest at rpf_step) also leave
       // its rpw pieces in flight
@@ -1254,11 +1261,13 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       if constexpr (HALO) {
         if (TP == 10 - STAGES && !last_blk) issue_halo(hw_blk_next, hw_buf_next);
       }
-      if (t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
+      if (STEADY || t + STAGES - 1 < nsteps) issue(t + STAGES - 1, (U + STAGES - 1) % STAGES);
       if constexpr (WIN) {
         if (TP == 0 && !last_blk) issue_win(w_j + 1, (w_j + 1) & 1);
       }
-      if (RPF && rpf_loop && t == rpf_step) issue_res(lds + rpf_off);
+      if constexpr (!STEADY) {
+        if (RPF && rpf_loop && t == rpf_step) issue_res(lds + rpf_off);
+      }
     };
     if constexpr (MODE == (int)Prec::F16) {
       half8 af[2][TI], bf[2][TJ];
@@ -1401,62 +1410,84 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
       hw_buf_next = (j + 1) & 1;
       const int t = j * 9;
       if constexpr (STAGES == 3) {
-        kstep(t + 0, I0{}, std::integral_constant<int, 0>{}, lb, Hs);
-        kstep(t + 1, I1{}, std::integral_constant<int, 1>{}, lb, Hs);
-        kstep(t + 2, I2{}, std::integral_constant<int, 2>{}, lb, Hs);
-        kstep(t + 3, I0{}, std::integral_constant<int, 3>{}, lb, Hs);
-        kstep(t + 4, I1{}, std::integral_constant<int, 4>{}, lb, Hs);
-        kstep(t + 5, I2{}, std::integral_constant<int, 5>{}, lb, Hs);
-        kstep(t + 6, I0{}, std::integral_constant<int, 6>{}, lb, Hs);
-        kstep(t + 7, I1{}, std::integral_constant<int, 7>{}, lb, Hs);
-        kstep(t + 8, I2{}, std::integral_constant<int, 8>{}, lb, Hs);
+        kstep(t + 0, I0{}, std::integral_constant<int, 0>{}, lb, Hs, std::false_type{});
+        kstep(t + 1, I1{}, std::integral_constant<int, 1>{}, lb, Hs, std::false_type{});
+        kstep(t + 2, I2{}, std::integral_constant<int, 2>{}, lb, Hs, std::false_type{});
+        kstep(t + 3, I0{}, std::integral_constant<int, 3>{}, lb, Hs, std::false_type{});
+        kstep(t + 4, I1{}, std::integral_constant<int, 4>{}, lb, Hs, std::false_type{});
+        kstep(t + 5, I2{}, std::integral_constant<int, 5>{}, lb, Hs, std::false_type{});
+        kstep(t + 6, I0{}, std::integral_constant<int, 6>{}, lb, Hs, std::false_type{});
+        kstep(t + 7, I1{}, std::integral_constant<int, 7>{}, lb, Hs, std::false_type{});
+        kstep(t + 8, I2{}, std::integral_constant<int, 8>{}, lb, Hs, std::false_type{});
       } else {
         auto nx = [&] {
           const int v = u;
           u = u + 1 == STAGES ? 0 : u + 1;
           return v;
         };
-        kstep(t + 0, nx(), std::integral_constant<int, 0>{}, lb, Hs);
-        kstep(t + 1, nx(), std::integral_constant<int, 1>{}, lb, Hs);
-        kstep(t + 2, nx(), std::integral_constant<int, 2>{}, lb, Hs);
-        kstep(t + 3, nx(), std::integral_constant<int, 3>{}, lb, Hs);
-        kstep(t + 4, nx(), std::integral_constant<int, 4>{}, lb, Hs);
-        kstep(t + 5, nx(), std::integral_constant<int, 5>{}, lb, Hs);
-        kstep(t + 6, nx(), std::integral_constant<int, 6>{}, lb, Hs);
-        kstep(t + 7, nx(), std::integral_constant<int, 7>{}, lb, Hs);
-        kstep(t + 8, nx(), std::integral_constant<int, 8>{}, lb, Hs);
+        kstep(t + 0, nx(), std::integral_constant<int, 0>{}, lb, Hs, std::false_type{});
+        kstep(t + 1, nx(), std::integral_constant<int, 1>{}, lb, Hs, std::false_type{});
+        kstep(t + 2, nx(), std::integral_constant<int, 2>{}, lb, Hs, std::false_type{});
+        kstep(t + 3, nx(), std::integral_constant<int, 3>{}, lb, Hs, std::false_type{});
+        kstep(t + 4, nx(), std::integral_constant<int, 4>{}, lb, Hs, std::false_type{});
+        kstep(t + 5, nx(), std::integral_constant<int, 5>{}, lb, Hs, std::false_type{});
+        kstep(t + 6, nx(), std::integral_constant<int, 6>{}, lb, Hs, std::false_type{});
+        kstep(t + 7, nx(), std::integral_constant<int, 7>{}, lb, Hs, std::false_type{});
+        kstep(t + 8, nx(), std::integral_constant<int, 8>{}, lb, Hs, std::false_type{});
       }
     }
   } else if constexpr (WIN) {
     // one super-step (kh, channel block) per iteration, its three kw taps unrolled: the W
     // stage is kw (slices start at a multiple of 3 steps), the window buffer j & 1
+    // (every super-step but the last one is steady: constant waits, no residual prefetch)
     const int ns = nsteps / 3;
-    for (int j = 0; j < ns; ++j) {
+    for (int j = 0; j < ns - 1; ++j) {
       const char* Ws = lds + STAGES * IMG + (j & 1) * HBUF;
       w_tap0 = ((w_g0 + j) >> w_nbs) * 3;
       w_j = j;
-      const bool lb = j == ns - 1;
-      kstep(3 * j, I0{}, I0{}, lb, Ws);
-      kstep(3 * j + 1, I1{}, I1{}, lb, Ws);
-      kstep(3 * j + 2, I2{}, I2{}, lb, Ws);
+      kstep(3 * j, I0{}, I0{}, false, Ws, std::true_type{});
+      kstep(3 * j + 1, I1{}, I1{}, false, Ws, std::true_type{});
+      kstep(3 * j + 2, I2{}, I2{}, false, Ws, std::true_type{});
+    }
+    {
+      const int j = ns - 1;
+      const char* Ws = lds + STAGES * IMG + (j & 1) * HBUF;
+      w_tap0 = ((w_g0 + j) >> w_nbs) * 3;
+      w_j = j;
+      kstep(3 * j, I0{}, I0{}, true, Ws, std::false_type{});
+      kstep(3 * j + 1, I1{}, I1{}, true, Ws, std::false_type{});
+      kstep(3 * j + 2, I2{}, I2{}, true, Ws, std::false_type{});
     }
   } else if constexpr (TAP) {
     // unrolled by STAGES: stage offsets are immediates (the conv loop is short;
     // unrolling the large dense-GEMM bodies measured 1-2 % slower end to end)
+    // steady iterations while every step of the iteration issues a step (t + 2 STAGES - 2 <
+    // nsteps), then the checked ones
+    using S1 = std::true_type;
+    using S0 = std::false_type;
     int t = 0;
-    for (; t + STAGES <= nsteps; t += STAGES) {
-      kstep(t, I0{}, I0{}, false, nullptr);
-      kstep(t + 1, I1{}, I0{}, false, nullptr);
-      if constexpr (STAGES > 2) kstep(t + 2, I2{}, I0{}, false, nullptr);
-      if constexpr (STAGES > 3) kstep(t + 3, I3{}, I0{}, false, nullptr);
+    for (; t + 2 * STAGES - 1 <= nsteps; t += STAGES) {
+      kstep(t, I0{}, I0{}, false, nullptr, S1{});
+      kstep(t + 1, I1{}, I0{}, false, nullptr, S1{});
+      if constexpr (STAGES > 2) kstep(t + 2, I2{}, I0{}, false, nullptr, S1{});
+      if constexpr (STAGES > 3) kstep(t + 3, I3{}, I0{}, false, nullptr, S1{});
     }
-    if (t < nsteps) kstep(t, I0{}, I0{}, false, nullptr);
+    for (; t + STAGES <= nsteps; t += STAGES) {
+      kstep(t, I0{}, I0{}, false, nullptr, S0{});
+      kstep(t + 1, I1{}, I0{}, false, nullptr, S0{});
+      if constexpr (STAGES > 2) kstep(t + 2, I2{}, I0{}, false, nullptr, S0{});
+      if constexpr (STAGES > 3) kstep(t + 3, I3{}, I0{}, false, nullptr, S0{});
+    }
+    if (t < nsteps) kstep(t, I0{}, I0{}, false, nullptr, S0{});
     if constexpr (STAGES > 2)
-      if (t + 1 < nsteps) kstep(t + 1, I1{}, I0{}, false, nullptr);
+      if (t + 1 < nsteps) kstep(t + 1, I1{}, I0{}, false, nullptr, S0{});
     if constexpr (STAGES > 3)
-      if (t + 2 < nsteps) kstep(t + 2, I2{}, I0{}, false, nullptr);
+      if (t + 2 < nsteps) kstep(t + 2, I2{}, I0{}, false, nullptr, S0{});
   } else {
-    for (int t = 0; t < nsteps; ++t) kstep(t, t % STAGES, I0{}, false, nullptr);
+    // steady while step t + STAGES - 1 exists (then t < rpf_step too)
+    int t = 0;
+    for (; t + STAGES - 1 < nsteps; ++t) kstep(t, t % STAGES, I0{}, false, nullptr, std::true_type{});
+    for (; t < nsteps; ++t) kstep(t, t % STAGES, I0{}, false, nullptr, std::false_type{});
   }
 
   SPI_STAMP(st_d);
@@ -1482,50 +1513,46 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   if constexpr (kSplitK<BM, BN, KIND>) {
 
   // ---- split-K: the last slice to arrive reduces -----------------------------
-  // Tickets first: a slice that is not last publishes its slab write-through (sc1) in
-  // fragment order (thread tid's accumulator (i, j) is 16 contiguous bytes at
-  // ((i*TJ + j)*NT + tid)*16), drains its stores (vmcnt(0)), and one lane counts the slab
-  // in a second word with a relaxed agent-scope atomic.  The last arriver keeps its own
-  // partial in registers -- no slab store, no read-back -- prefetches the residual,
-  // polls the count (sc1 loads) until every other slab is published, resets both words,
-  // and reads the slabs with sc1 loads (MI355X_MICROARCH.md, the sc1 hand-off).  Every
-  // slice that is not last took its ticket after its k-loop, so the poll ends.  Partials
-  // are summed in split order whichever slice arrives last: deterministic results.
+  // Every slice publishes its slab write-through (sc1) in fragment order (thread tid's
+  // accumulator (i, j) is 16 contiguous bytes at ((i*TJ + j)*NT + tid)*16), drains its stores
+  // (vmcnt(0)) and takes a relaxed agent-scope ticket; the last to arrive resets the ticket,
+  // prefetches the residual, reads the other slabs with sc1 loads (MI355X_MICROARCH.md, the
+  // sc1 hand-off) and adds its own partial from registers.  (Round 4 tried tickets first --
+  // only the non-last slices store, the last one polls a published-slab count: the poll made
+  // the reducer ~1.2 us slower, tools/gemm_timeline.py.)  Partials are summed in split order
+  // whichever slice arrives last: deterministic results.
   const int splits = a.splits;
   constexpr int SLAB = BM * BN;
-  int* words = a.p.counters + 2 * tile;  // [0] arrival ticket, [1] published slabs
+  int* words = a.p.counters + 2 * tile;  // [0] arrival ticket ([1] unused)
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(tile_slabs, (short)0, splits * SLAB * 4, 0x00020000);
-  if (tid == 0) *s_flag = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
+    }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (tid == 0) {
+    const int ticket = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == splits - 1;
+    if (last) __hip_atomic_store(words, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
   __syncthreads();
-  if (*s_flag < splits - 1) {
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int off = (kslice * SLAB + ((i * TJ + j) * NT + tid) * 4) * 4;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16);
-      }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (tid == 0) __hip_atomic_fetch_add(words + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!*s_flag) {
     tl_out(1);
     return;
   }
   const bool rpf_red = RPF && rpf_tile;
   char* const red_res = lds + (WIN ? STAGES * IMG : IMG);  // the parked tile takes [0, BM * BN * 4)
   if (rpf_red) issue_res(red_res);
-  if (tid == 0) {
-    while (__hip_atomic_load(words + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
-      __builtin_amdgcn_s_sleep(1);
-    __hip_atomic_store(words, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(words + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
   // ZR splits' slabs in flight per round (two for the small tiles, one when a slab is 8+
   // fragments per thread); loads past the last slab fall outside the descriptor's range and
-  // return 0 (no branch, no per-load wait); this slice's own slot (never written) is
-  // loaded and ignored.
+  // return 0 (no branch, no per-load wait); this slice's own slot is loaded and ignored (its
+  // partial is still in registers).
   constexpr int ZR = TI * TJ <= 4 ? 2 : 1;
   floatx4 sum[TI][TJ];
 #pragma unroll
@@ -1612,6 +1639,10 @@ struct Knobs {
   // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
   // GEMMs stay off: -1.3 % with them)
   int g256_longk_tiles = 48, g256_longk_k = 1024;
+  // SPI_GEMM_256_LONGK="tiles,K,S": gemm256 split-K up to S slices for grids under T tiles (default
+  // 1: none -- round 4 measured ViT-L FFN2 at 3 slices 100 -> 73 us back to back but C5 under the
+  // four streams 6.05k -> 5.09k inf/s: the slices' CU-time and slab traffic cost the other streams more)
+  int g256_split = 1;
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
   struct HaloPick {
@@ -1644,10 +1675,11 @@ Knobs read_knobs() {
     k.target = std::max(1, std::atoi(e + 5));
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
   if (const char* e = std::getenv("SPI_GEMM_256_LONGK"); e && *e) {
-    int t = 0, kk = 0;
-    if (std::sscanf(e, "%d,%d", &t, &kk) == 2) {
+    int t = 0, kk = 0, sp = 1;
+    if (std::sscanf(e, "%d,%d,%d", &t, &kk, &sp) >= 2) {
       k.g256_longk_tiles = t;
       k.g256_longk_k = kk;
+      k.g256_split = std::max(1, sp);
     } else {
       k.g256_longk_tiles = 0;  // e.g. "0": off
     }
@@ -1692,7 +1724,11 @@ bool routes_256(const GemmDesc& d, Prec prec) {
                                (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k &&
                                 gemm256_eligible(d, prec, k.g256_longk_tiles)));
 }
-int g256_splits(const GemmDesc& d) { return gemm256_splits(d, knobs().target, knobs().max_split); }
+int g256_splits(const GemmDesc& d) {
+  const Knobs& k = knobs();
+  const int cap = k.max_split > 0 ? std::min(k.max_split, k.g256_split) : k.g256_split;
+  return cap > 1 ? gemm256_splits(d, k.target, cap) : 1;
+}
 
 Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
   const Knobs& k = knobs();

@@ -424,12 +424,14 @@ def test_gemm256_in_place_residual(ops, gemm256_everywhere, router, M, N, K):
 @pytest.mark.parametrize("maxsplit", ["1", "2", "3", "0"])
 @pytest.mark.parametrize("M,N,K,res", [(600, 512, 4096, "f32"), (3152, 1024, 2048, None), (257, 256, 3072, "f16")])
 def test_gemm256_split_k(ops, gemm256_everywhere, maxsplit, M, N, K, res):
-    """gemm256's split-K (grids under 128 workgroups: slices of >= 16 k-tiles, at most 4; the
+    """gemm256's split-K (opt-in, SPI_GEMM_256_LONGK's third field; grids under 128 workgroups:
+    slices of >= 16 k-tiles, at most 4; the
     last slice to arrive sums the write-through slabs in slice order).  SPI_GEMM_MAXSPLIT caps
     the slices (0 = uncapped: 4 for 600x512x4096, 2 for 3152x1024x2048, 3 for 257x256x3072;
     a cap of 3 on the first gives a short last slice).  The sum order does not depend on
     arrival: two launches agree bit for bit."""
     import os
+    os.environ["SPI_GEMM_256_LONGK"] = "48,1024,4"  # split-K is opt-in (third field: slices)
     os.environ["SPI_GEMM_MAXSPLIT"] = maxsplit
     ops.lib.spi_debug_gemm_reload_env()
     try:
@@ -450,6 +452,7 @@ def test_gemm256_split_k(ops, gemm256_everywhere, maxsplit, M, N, K, res):
         assert torch.equal(outs[0], outs[1]), "split-K sums depend on arrival order"
     finally:
         os.environ.pop("SPI_GEMM_MAXSPLIT", None)
+        os.environ.pop("SPI_GEMM_256_LONGK", None)
         ops.lib.spi_debug_gemm_reload_env()
 
 

@@ -21,7 +21,8 @@ RESNET18 = [(8, 224, 8, 64, 7, 2, False), (8, 56, 64, 64, 3, 1, False), (8, 56, 
             (8, 56, 64, 128, 3, 2, False), (8, 28, 128, 128, 3, 1, True), (8, 56, 64, 128, 1, 2, False),
             (8, 28, 128, 256, 3, 2, False), (8, 14, 256, 256, 3, 1, True), (8, 14, 256, 512, 3, 2, False),
             (8, 7, 512, 512, 3, 1, True)]
-GEMMS = [(1024, 3072, 768), (1024, 768, 3072), (3152, 3072, 1024), (4096, 4096, 4096)]
+GEMMS = [(1024, 3072, 768), (1024, 768, 3072), (3152, 3072, 1024), (3152, 4096, 1024), (3152, 1024, 4096),
+         (3152, 1024, 1024), (4096, 4096, 4096)]
 
 
 def load(path):
