@@ -72,6 +72,12 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMaxSplits = 4;     // split-K slices (gemm256_splits)
 constexpr int kMinSliceKt = 16;   // k-tiles per slice at least (ViT-L out-proj, K = 1024, 2 x 8: 52.9 us b2b vs 40.2 unsplit)
 constexpr int kBufBytes = 65536;  // one k-tile: A 256 x 128 B + B 256 x 128 B
+// diagnostic build -DSPI_G256_EPI_CALLS: leave the epilogue instances to the inliner (A/B)
+#ifdef SPI_G256_EPI_CALLS
+#define SPI_G256_EPI_INLINE
+#else
+#define SPI_G256_EPI_INLINE __attribute__((always_inline))
+#endif
 constexpr int kBOff = 32768;
 
 // 8-row piece base (tile row) of piece pc (0..15) of quarter q
@@ -399,7 +405,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // activation and output format are dispatched once, outside the rounds (always_inline: left
   // to itself hipcc outlined the 12 instances as calls, spilling the accumulators -- 944 bytes of
   // scratch per thread -- around each)
-  auto epi = [&](auto act_c, auto f32_c, auto guard_c) __attribute__((always_inline)) {
+  auto epi = [&](auto act_c, auto f32_c, auto guard_c) SPI_G256_EPI_INLINE {
     constexpr int ACT = decltype(act_c)::value;
     constexpr bool OUTF32 = decltype(f32_c)::value;
     constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
@@ -528,13 +534,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 };
-  auto by_guard = [&](auto act_c, auto f32_c) __attribute__((always_inline)) {
+  auto by_guard = [&](auto act_c, auto f32_c) SPI_G256_EPI_INLINE {
     if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
       epi(act_c, f32_c, std::false_type{});
     else
       epi(act_c, f32_c, std::true_type{});
   };
-  auto by_act = [&](auto f32_c) __attribute__((always_inline)) {
+  auto by_act = [&](auto f32_c) SPI_G256_EPI_INLINE {
     if (act == Act::Gelu)
       by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
     else if (act == Act::Relu)

@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--set", default="all", choices=["resnet18", "gemm", "all"])
     ap.add_argument("--env-a", default="", help="knobs for lib A only, e.g. 'SPI_GEMM_NG=2' (comma-separated)")
     ap.add_argument("--env-b", default="", help="knobs for lib B only")
+    ap.add_argument("--act", type=int, default=0, help="GEMM activation: 0 none, 1 relu, 2 gelu")
+    ap.add_argument("--out16", action="store_true", help="GEMMs: fp16 output (the transformer epilogues)")
     a = ap.parse_args()
     if a.libs[0] == a.libs[1]:  # same file twice: load a private copy so each keeps its own knobs
         import shutil
@@ -123,9 +125,12 @@ def main():
             for M, N, K in GEMMS:
                 A = act(M, K)
                 wp = packed(libs[0], prec, N, K)
-                outs = [torch.empty_like(act(M, N)) if split else torch.empty(M, N, device="cuda") for _ in libs]
-                fns = [(lambda l=l, o=o, w=w: l.spi_op_gemm(prec, A.data_ptr(), M, K, K, wp.data_ptr(), N, None, None,
-                                                           0, 0, o.data_ptr(), 0 if split else 1, N, 0, w.data_ptr(), s))
+                o16 = split or a.out16
+                outs = [torch.empty_like(act(M, N)) if o16 else torch.empty(M, N, device="cuda") for _ in libs]
+                bias = torch.randn(N, device="cuda")
+                fns = [(lambda l=l, o=o, w=w: l.spi_op_gemm(prec, A.data_ptr(), M, K, K, wp.data_ptr(), N, bias.data_ptr(),
+                                                           None, 0, 0, o.data_ptr(), 0 if o16 else 1, N, a.act,
+                                                           w.data_ptr(), s))
                        for l, o, w in zip(libs, outs, ws)]
                 t = time_pair(fns)
                 print(f"{pname:6s} gemm {M}x{N}x{K}: A {t[0]:.2f} us ({2 * M * N * K / t[0] / 1e6:.0f} TF/s)  "
