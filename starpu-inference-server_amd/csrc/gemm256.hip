@@ -129,9 +129,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // ONE LDS object: with a second __shared__ variable beside the k-tile buffers hipcc's waitcnt
   // pass could no longer tell the LDS-DMA destinations from the fragment reads and put a
   // vmcnt(0) in front of every phase's reads (ViT-L FFN1 / QKV +15 %, round 4)
+#ifdef SPI_G256_LDS128  // diagnostic: exactly the k-tile buffers + the ticket (no LayerNorm statistics)
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes + 16];
+  float2* const ln_s = reinterpret_cast<float2*>(lds);
+  int* const s_ticket = reinterpret_cast<int*>(lds + 2 * kBufBytes);
+#else
   __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes + 256 * 8 + 16];
   float2* const ln_s = reinterpret_cast<float2*>(lds + 2 * kBufBytes);  // LayerNorm fold: tile rows' {mean, rstd}
   int* const s_ticket = reinterpret_cast<int*>(lds + 2 * kBufBytes + 256 * 8);
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
