@@ -129,15 +129,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // ONE LDS object: with a second __shared__ variable beside the k-tile buffers hipcc's waitcnt
   // pass could no longer tell the LDS-DMA destinations from the fragment reads and put a
   // vmcnt(0) in front of every phase's reads (ViT-L FFN1 / QKV +15 %, round 4)
-#ifdef SPI_G256_LDS128  // diagnostic: exactly the k-tile buffers + the ticket (no LayerNorm statistics)
-  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes + 16];
-  float2* const ln_s = reinterpret_cast<float2*>(lds);
-  int* const s_ticket = reinterpret_cast<int*>(lds + 2 * kBufBytes);
-#else
-  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes + 256 * 8 + 16];
-  float2* const ln_s = reinterpret_cast<float2*>(lds + 2 * kBufBytes);  // LayerNorm fold: tile rows' {mean, rstd}
-  int* const s_ticket = reinterpret_cast<int*>(lds + 2 * kBufBytes + 256 * 8);
-#endif
+  // and exactly the two k-tile buffers: 2 KiB more (the LayerNorm statistics, round 4) made
+  // every launch 2-5 % slower (tools/ab_gemm.py, -DSPI_G256_LDS128 against it).  The split-K
+  // ticket lives in buffer 0 once the k-loop's last reads are done; the statistics in registers.
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
+  int* const s_ticket = reinterpret_cast<int*>(lds);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
@@ -384,7 +380,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   float* T = reinterpret_cast<float*>(lds);
   const int cg = tid & 31, r0 = tid >> 5;  // 8-column group, first row of this thread
   // the tile rows' LayerNorm statistics, once per row (read after round 0's park barrier)
-  if (g.ln_in_chunks > 0) ln_tile_stats(g.ln_in_stats, m0, 256, g.M, g.ln_in_chunks, g.ln_in_eps, ln_s, tid, 512);
+  // LayerNorm fold: the walk's row of pass p in round h is m0 + 128 h + r0 + 16 p, shared by the 32
+  // lanes of this thread's half-wave; lane cg computes {mean, rstd} of pass cg & 7's row in both
+  // rounds (all chunk loads in flight), and the walk takes them from lane (lane & 32) | p
+  float2 ln_st[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
+  if (g.ln_in_chunks > 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float mean, rstd;
+      ln_row_stats(g.ln_in_stats, min(m0 + 128 * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks, g.ln_in_eps,
+                   mean, rstd);
+      ln_st[h] = float2{mean, rstd};
+    }
+  }
   const int nb = n0 + 8 * cg;
   float bias8[8], c18[8];
   if (g.ln_in_chunks > 0) {
@@ -489,9 +497,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] = e < 4 ? x0[e] : x1[e - 4];
           if (g.ln_in_chunks > 0) {  // LayerNorm of the A rows folded in: rstd (acc - mean c1)
-            const float2 st = ln_s[128 * h + row];
+            const int src = (lane & 32) | pass;
+            const float mean = __shfl(ln_st[h].x, src, 64), rstd = __shfl(ln_st[h].y, src, 64);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) y[e] = st.y * (y[e] - st.x * c18[e]);
+            for (int e = 0; e < 8; ++e) y[e] = rstd * (y[e] - mean * c18[e]);
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
