@@ -379,31 +379,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // hides behind it.
   float* T = reinterpret_cast<float*>(lds);
   const int cg = tid & 31, r0 = tid >> 5;  // 8-column group, first row of this thread
-  // the tile rows' LayerNorm statistics, once per row (read after round 0's park barrier)
-  // LayerNorm fold: the walk's row of pass p in round h is m0 + 128 h + r0 + 16 p, shared by the 32
-  // lanes of this thread's half-wave; lane cg computes {mean, rstd} of pass cg & 7's row in both
-  // rounds (all chunk loads in flight), and the walk takes them from lane (lane & 32) | p
-  float2 ln_st[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  if (g.ln_in_chunks > 0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float mean, rstd;
-      ln_row_stats(g.ln_in_stats, min(m0 + 128 * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks, g.ln_in_eps,
-                   mean, rstd);
-      ln_st[h] = float2{mean, rstd};
-    }
-  }
   const int nb = n0 + 8 * cg;
-  float bias8[8], c18[8];
-  if (g.ln_in_chunks > 0) {
-    const floatx4 c0 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb);
-    const floatx4 c1 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      c18[e] = c0[e];
-      c18[e + 4] = c1[e];
-    }
-  }
+  float bias8[8];
   if (g.bias) {
     const floatx4 b0 = *reinterpret_cast<const floatx4*>(g.bias + nb);
     const floatx4 b1 = *reinterpret_cast<const floatx4*>(g.bias + nb + 4);
@@ -419,10 +396,34 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // activation and output format are dispatched once, outside the rounds (always_inline: left
   // to itself hipcc outlined the 12 instances as calls, spilling the accumulators -- 944 bytes of
   // scratch per thread -- around each)
-  auto epi = [&](auto act_c, auto f32_c, auto guard_c) SPI_G256_EPI_INLINE {
+  // LNC (compile-time: a launch without the fold carries none of its registers -- as a runtime
+  // branch it cost every gemm256 launch 2-5 %): the consumer side of the LayerNorm fold.  The
+  // walk's row of pass p in round h is m0 + 128 h + r0 + 16 p, shared by the 32 lanes of this
+  // thread's half-wave; lane cg computes {mean, rstd} of pass cg & 7's row in both rounds (all
+  // chunk loads in flight) and the walk takes them from lane (lane & 32) | p.
+  auto epi = [&](auto act_c, auto f32_c, auto guard_c, auto lnc_c) SPI_G256_EPI_INLINE {
     constexpr int ACT = decltype(act_c)::value;
     constexpr bool OUTF32 = decltype(f32_c)::value;
     constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
+    constexpr bool LNC = decltype(lnc_c)::value;
+    [[maybe_unused]] float2 ln_st[2];
+    [[maybe_unused]] float c18[8];
+    if constexpr (LNC) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float mean, rstd;
+        ln_row_stats(g.ln_in_stats, min(m0 + 128 * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks,
+                     g.ln_in_eps, mean, rstd);
+        ln_st[h] = float2{mean, rstd};
+      }
+      const floatx4 c0 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb);
+      const floatx4 c1 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        c18[e] = c0[e];
+        c18[e + 4] = c1[e];
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // residual rows: the first half of the round's prefetched, the rest loaded inside the
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           float y[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] = e < 4 ? x0[e] : x1[e - 4];
-          if (g.ln_in_chunks > 0) {  // LayerNorm of the A rows folded in: rstd (acc - mean c1)
+          if constexpr (LNC) {  // LayerNorm of the A rows folded in: rstd (acc - mean c1)
             const int src = (lane & 32) | pass;
             const float mean = __shfl(ln_st[h].x, src, 64), rstd = __shfl(ln_st[h].y, src, 64);
 #pragma unroll
@@ -549,24 +550,32 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 };
-  auto by_guard = [&](auto act_c, auto f32_c) SPI_G256_EPI_INLINE {
+  auto by_guard = [&](auto act_c, auto f32_c, auto lnc_c) SPI_G256_EPI_INLINE {
     if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
-      epi(act_c, f32_c, std::false_type{});
+      epi(act_c, f32_c, std::false_type{}, lnc_c);
     else
-      epi(act_c, f32_c, std::true_type{});
+      epi(act_c, f32_c, std::true_type{}, lnc_c);
   };
-  auto by_act = [&](auto f32_c) SPI_G256_EPI_INLINE {
+  auto by_act = [&](auto f32_c, auto lnc_c) SPI_G256_EPI_INLINE {
     if (act == Act::Gelu)
-      by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c, lnc_c);
     else if (act == Act::Relu)
-      by_guard(std::integral_constant<int, (int)Act::Relu>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::Relu>{}, f32_c, lnc_c);
     else
-      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c);
+      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c, lnc_c);
   };
+  // the consumer fold exists for fp16 outputs without a residual (the QKV / FFN1 GEMMs; checked
+  // on the host)
+  if constexpr (RES == 0) {
+    if (g.ln_in_chunks > 0) {
+      by_act(std::false_type{}, std::true_type{});
+      return;
+    }
+  }
   if (g.out_f32)
-    by_act(std::true_type{});
+    by_act(std::true_type{}, std::false_type{});
   else
-    by_act(std::false_type{});
+    by_act(std::false_type{}, std::false_type{});
 }
 
 }  // namespace
@@ -626,6 +635,8 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
   g.c16 = p.ln.c16;
   if ((d.ln_in_chunks > 0 || d.ln_out) && !g.vec_ok)
     throw std::invalid_argument("gemm256: the LayerNorm fold needs the vector epilogue");
+  if (d.ln_in_chunks > 0 && (p.res || d.out_f32))
+    throw std::invalid_argument("gemm256: the LayerNorm consumer fold is for fp16 outputs without a residual");
   if (d.res_ln_chunks > 0) throw std::invalid_argument("gemm256: no residual LayerNorm (post-LN) epilogue");
   const int kt = d.K / 64;
   g.ktp = (kt + splits - 1) / splits;
