@@ -181,6 +181,7 @@ def test_transformer_layernorm_fold(spi, zoo, gpu, family, monkeypatch):
         m = zoo.vit(image=224, patch=16, layers=3, heads=2, dim=128, mlp_dim=256)
         inputs, kw = [image(rng, 2, 224)], dict(max_batch=2)
     ref = cpu_inference(m, inputs)[0]
+    monkeypatch.setenv("SPI_LN_FOLD", "1")  # whatever the family's default
     rep = spi.ModelReplica(m, 0, "fp16", **kw)
     folded = hip_forward(spi, rep, inputs, ref.shape, graphs=True)
     ins = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in inputs]
