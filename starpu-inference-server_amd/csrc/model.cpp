@@ -277,9 +277,11 @@ bool ln_fold_enabled(Prec prec, bool by_default) {
   const bool on = (e && *e) ? std::atoi(e) != 0 : by_default;
   return prec == Prec::F16 && on;
 }
-// BERT-base: fold +3.9 % four-stream (same process, round 4); ViT-L: see kVitLnFold
+// BERT-base: fold +3.9 % four-stream (same process, round 4).  ViT-L: 5.93k with it against 6.30k
+// without (same process, profiles/r04/fixed/vit_fold_ab.txt): its long GEMMs gain less from the
+// removed launches than the producer epilogues (statistics + fp16 copy) cost them
 constexpr bool kBertLnFold = true;
-constexpr bool kVitLnFold = true;
+constexpr bool kVitLnFold = false;
 
 LnW pack_ln(const PMap& p, const std::string& name) {
   LnW l;
