@@ -81,6 +81,52 @@ def read_launches(path):
     return by_key
 
 
+def strip_args(k: str) -> str:
+    """A kernel key without its template arguments (demangled '<...>' or mangled 'I...E')."""
+    k = k.split("<", 1)[0]
+    m = re.match(r"([A-Za-z_][A-Za-z0-9_]*?)I(L[ib].*)?$", k)
+    return m.group(1) if m else k
+
+
+def read_table(path):
+    """The launch table as a list of (op, kernel name without template args, gx, gy)."""
+    rows = []
+    with open(path) as f:
+        for line in f:
+            if not line.strip() or line.startswith("#"):
+                continue
+            idx, name, kernel, gx, gy, gz, block = line.rstrip("\n").split("\t")
+            rows.append((name, strip_args(base_key(kernel)), int(gx), int(gy)))
+    return rows
+
+
+def attribute_by_sequence(dispatches, table):
+    """Op of every dispatch by walking each hardware queue's dispatches (start-time order) along
+    the launch table: one forward's launch sequence, replayed back to back by every worker
+    stream.  Kernel names alone cannot tell two launches of one template instance and grid apart
+    (ViT-L's out-proj and FFN2: the same gemm256 instance on 52 workgroups), their position in
+    the forward can.  A dispatch that does not fit the next table entry resynchronises on the
+    nearest entry it fits (warm-up copies and fills fit none: left unattributed)."""
+    n = len(table)
+    by_q = collections.defaultdict(list)
+    for i, d in enumerate(dispatches):
+        by_q[d["queue"]].append(i)
+    ops = [""] * len(dispatches)
+    for q, idx in by_q.items():
+        idx.sort(key=lambda i: dispatches[i]["start"])
+        p = 0
+        for i in idx:
+            d = dispatches[i]
+            key = (d["name"], d["gx"], d["gy"])
+            for step in range(n):
+                j = (p + step) % n
+                if table[j][1:] == key:
+                    ops[i] = table[j][0]
+                    p = (j + 1) % n
+                    break
+    return ops
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -88,23 +134,35 @@ def main():
     ap.add_argument("--top", type=int, default=20)
     ap.add_argument("--csv", default="", help="write the table here as CSV")
     a = ap.parse_args()
-    groups = collections.defaultdict(list)
-    names = {}
+    dispatches = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
             wg = int(r["Workgroup_Size_X"])
-            key = (base_key(r["Kernel_Name"]), int(r["Grid_Size_X"]) // max(wg, 1), int(r["Grid_Size_Y"]))
-            names.setdefault(key, r["Kernel_Name"])
-            groups[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            k = base_key(r["Kernel_Name"])
+            dispatches.append(dict(key=k, name=strip_args(k), gx=int(r["Grid_Size_X"]) // max(wg, 1),
+                                   gy=int(r["Grid_Size_Y"]), start=int(r["Start_Timestamp"]),
+                                   queue=r.get("Queue_Id") or r.get("Stream_Id") or "0",
+                                   us=(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     launches = read_launches(a.launches) if a.launches else {}
+    table = read_table(a.launches) if a.launches else []
+    # the table's kernel ids carry no template arguments (clang's __PRETTY_FUNCTION__ prints the
+    # specialisation's name only): attribute by position in the forward instead
+    seq_ops = attribute_by_sequence(dispatches, table) if table else [""] * len(dispatches)
+    per_fwd_of = collections.Counter(t[0] for t in table)
+    groups = collections.defaultdict(list)
+    for d, op in zip(dispatches, seq_ops):
+        groups[(op, d["key"], d["gx"], d["gy"])].append(d["us"])
     rows = []
     total_all = sum(sum(d) for d in groups.values())
-    for (kname, gx, gy), d in groups.items():
+    for (op, kname, gx, gy), d in groups.items():
         d.sort()
         q = lambda p: d[min(len(d) - 1, int(p * (len(d) - 1)))]
-        ops = launches.get((kname, gx, gy), {})
-        op = "|".join(sorted(ops)) if ops else ""
-        per_fwd = sum(ops.values()) if ops else 0
+        if not op:  # fall back to the (kernel, grid) match of a table with template arguments
+            ops = launches.get((kname, gx, gy), {})
+            op = "|".join(sorted(ops)) if ops else ""
+            per_fwd = sum(ops.values()) if ops else 0
+        else:
+            per_fwd = per_fwd_of[op]
         rows.append((op, kname, gx, gy, per_fwd, len(d), sum(d), sum(d) / total_all, statistics.mean(d),
                      statistics.median(d), q(0.1), q(0.9)))
     rows.sort(key=lambda x: -x[6])
