@@ -11,10 +11,12 @@
 set -euo pipefail
 export TMPDIR=/tmp
 cfgs=(resnet18:8:fp16m bert_base:8:fp16 resnet152:32:fp16x3 vit_l_16:16:fp16)
-mkdir -p gpurun_out/trace
-bash tools/trace_round.sh "${cfgs[@]}" > gpurun_out/trace/log.txt 2>&1
-mkdir -p profiles/r04
-cp gpurun_out/trace/trace_*_ops.csv profiles/r04/
+if [ "${SKIP_TRACE:-0}" != 1 ]; then  # SKIP_TRACE=1: the committed profiles/r04 traces pick the ops
+  mkdir -p gpurun_out/trace
+  bash tools/trace_round.sh "${cfgs[@]}" > gpurun_out/trace/log.txt 2>&1
+  mkdir -p profiles/r04
+  cp gpurun_out/trace/trace_*_ops.csv profiles/r04/
+fi
 out=gpurun_out/rl4
 mkdir -p "$out"
 for c in "${cfgs[@]}"; do
@@ -33,7 +35,8 @@ EOF
     python3 bench.py --roofline-only --roofline-op "$op" --model "$model" --batch "$batch" --precision "$prec" \
     > "$out/${tag}_roofline.json" 2> "$out/${tag}_roofline.err"
   stats=$(ls "$out/$tag"/*/*_kernel_stats.csv | head -n 1)
-  python3 tools/rocprof_roofline.py "$stats" "$op" "$out/roofline_rocprof.json"
+  ktrace=$(ls "$out/$tag"/*/*_kernel_trace.csv | head -n 1)
+  python3 tools/rocprof_roofline.py "$stats" "$op" "$out/roofline_rocprof.json" "$ktrace"
   cp "$stats" "$out/roofline_${tag}_kernel_stats.csv"
   rm -rf "$out/$tag"
 done
