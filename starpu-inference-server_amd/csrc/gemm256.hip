@@ -401,11 +401,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   // walk's row of pass p in round h is m0 + 128 h + r0 + 16 p, shared by the 32 lanes of this
   // thread's half-wave; lane cg computes {mean, rstd} of pass cg & 7's row in both rounds (all
   // chunk loads in flight) and the walk takes them from lane (lane & 32) | p.
-  auto epi = [&](auto act_c, auto f32_c, auto guard_c, auto lnc_c) SPI_G256_EPI_INLINE {
+  // LNO (compile-time too): the producer side (chunk statistics + the fp16 copy of every row).
+  auto epi = [&](auto act_c, auto f32_c, auto guard_c, auto lnc_c, auto lno_c) SPI_G256_EPI_INLINE {
     constexpr int ACT = decltype(act_c)::value;
     constexpr bool OUTF32 = decltype(f32_c)::value;
     constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
     constexpr bool LNC = decltype(lnc_c)::value;
+    constexpr bool LNO = decltype(lno_c)::value;
     [[maybe_unused]] float2 ln_st[2];
     [[maybe_unused]] float c18[8];
     if constexpr (LNC) {
@@ -521,7 +523,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           // could, races with the real row M - 1 when C is the residual buffer itself -- the
           // transformer's in-place residual stream: a duplicate that reads the residual after the
           // real row's store adds the GEMM twice.)
-          if (g.ln_out) {  // producer: chunk statistics (all lanes shuffle) + the fp16 copy
+          if constexpr (LNO) {  // producer: chunk statistics (all lanes shuffle) + the fp16 copy
             float mean, m2;
             ln_chunk_stats(y, mean, m2);
             if (m < g.M) {
@@ -550,32 +552,40 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 };
-  auto by_guard = [&](auto act_c, auto f32_c, auto lnc_c) SPI_G256_EPI_INLINE {
+  auto by_guard = [&](auto act_c, auto f32_c, auto lnc_c, auto lno_c) SPI_G256_EPI_INLINE {
     if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
-      epi(act_c, f32_c, std::false_type{}, lnc_c);
+      epi(act_c, f32_c, std::false_type{}, lnc_c, lno_c);
     else
-      epi(act_c, f32_c, std::true_type{}, lnc_c);
+      epi(act_c, f32_c, std::true_type{}, lnc_c, lno_c);
   };
-  auto by_act = [&](auto f32_c, auto lnc_c) SPI_G256_EPI_INLINE {
+  auto by_act = [&](auto f32_c, auto lnc_c, auto lno_c) SPI_G256_EPI_INLINE {
     if (act == Act::Gelu)
-      by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c, lnc_c);
+      by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c, lnc_c, lno_c);
     else if (act == Act::Relu)
-      by_guard(std::integral_constant<int, (int)Act::Relu>{}, f32_c, lnc_c);
+      by_guard(std::integral_constant<int, (int)Act::Relu>{}, f32_c, lnc_c, lno_c);
     else
-      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c, lnc_c);
+      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c, lnc_c, lno_c);
   };
-  // the consumer fold exists for fp16 outputs without a residual (the QKV / FFN1 GEMMs; checked
-  // on the host)
+  using F = std::false_type;
+  using T1 = std::true_type;
+  // the consumer fold exists for fp16 outputs without a residual (the QKV / FFN1 GEMMs), the
+  // producer for fp32 outputs over an fp32 residual (ViT's out-proj / FFN2); checked on the host
   if constexpr (RES == 0) {
     if (g.ln_in_chunks > 0) {
-      by_act(std::false_type{}, std::true_type{});
+      by_act(F{}, T1{}, F{});
+      return;
+    }
+  }
+  if constexpr (RES == 2) {
+    if (g.ln_out) {
+      by_act(T1{}, F{}, T1{});
       return;
     }
   }
   if (g.out_f32)
-    by_act(std::true_type{}, std::false_type{});
+    by_act(T1{}, F{}, F{});
   else
-    by_act(std::false_type{}, std::false_type{});
+    by_act(F{}, F{}, F{});
 }
 
 }  // namespace
@@ -637,6 +647,8 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
     throw std::invalid_argument("gemm256: the LayerNorm fold needs the vector epilogue");
   if (d.ln_in_chunks > 0 && (p.res || d.out_f32))
     throw std::invalid_argument("gemm256: the LayerNorm consumer fold is for fp16 outputs without a residual");
+  if (d.ln_out && (!p.res || !d.res_f32 || !d.out_f32))
+    throw std::invalid_argument("gemm256: the LayerNorm producer fold is for fp32 outputs over an fp32 residual");
   if (d.res_ln_chunks > 0) throw std::invalid_argument("gemm256: no residual LayerNorm (post-LN) epilogue");
   const int kt = d.K / 64;
   g.ktp = (kt + splits - 1) / splits;
