@@ -1828,7 +1828,7 @@ Plan halo_plan(const GemmDesc& d, Prec prec, int T) {
 // XCD rectangles (gemm_kernel's tile decode): the row x column group split
 // gm x gn (gm * gn = 8, the XCDs) that minimises the bytes the XCDs' L2s fetch,
 // A * gn + W * gm (A: the activation bytes a tile row block reads -- the input
-// image for convs; W: the packed weights).  SPI_GEMM_XCD2D=0: gm = 1.
+// image for convs; W: the packed weights).
 void xcd_groups(const GemmDesc& d, Prec prec, int TM, int TN, int& gm, int& gn) {
   gm = 1;
   gn = std::min(8, TN);

@@ -171,7 +171,7 @@ class Model {
   std::vector<int> stage_blocks_;
   ConvW stem_;
   bool stem_fused_ = false;  // stem + max pool in one launch on the NCHW input (stem.hip)
-  int stem_pr_ = 0;          // its workgroup shape (SPI_STEM_PR; 0 = auto, stem.hip)
+  int stem_pr_ = 0;          // its workgroup shape (0 = auto, stem.hip)
   size_t stem_pool_w_ = 0;   // its weights, [hi | lo][64][24][8] fp16
   std::vector<ResBlock> blocks_;
   LinearW fc_;

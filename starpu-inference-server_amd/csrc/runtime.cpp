@@ -822,8 +822,9 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
     // ResNet-50 (72), 0.949 ResNet-101 (38), 0.950 ResNet-152 (26); ViT-L (5) and BERT (0.1)
     // lose too.  The compute-bound side loses because the device's kernels run slower beside
     // the SDMA traffic, not because the worker waits for the copy: pinning the copies to a
-    // free engine (SPI_H2D_SDMA_ENGINE=high) cut ResNet-152's per-task copy wait from ~7 ms to
-    // ~1 ms and the rate still fell (9.2k vs 10.6k inf/s on the streams, tools/sdma_ab.py).
+    // free engine (a round-3 option, since removed) cut ResNet-152's per-task copy wait from ~7 ms
+    // to ~1 ms and the rate still fell (9.2k vs 10.6k inf/s on the streams); round 4 re-measured
+    // C4 / C5 at 10.1k / 4.56k on SDMA against 11.2k / 4.79k on the streams (tools/sdma_ab.py).
     // Below the threshold: a shared copy stream for <= 3 workers, the worker streams beyond
     // (four busy streams per device)
     size_t task_in = 0;
