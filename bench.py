@@ -812,6 +812,16 @@ def ci_perf_workload(spi, zoo, rtmod, dev, workers):
                       max_queue=100, slots_per_device=12, pipeline_depth=4, batching=b)
     out.update({"schedule_delta_us_repeat": sched, "expected_requests": 6300, "dtype": "fp16x3",
                 "config": "ci/perf/resnet152_ci_perf_gpu_only.yml (adaptive 1..16, queue 100, pool 12, pipeline 4)"})
+    # This build's MI355X tuning beside it: the same strategy and limits, but an idle worker
+    # dispatches what is queued at once instead of waiting out the 10 ms coalescer
+    # (spi_batching_config.idle_dispatch; batches still form while every worker is busy).
+    bt = rtmod.batching_config("adaptive", 1, 16, coalesce_timeout_us=10_000, congestion=True, tick_us=500_000,
+                               entry_horizon_us=3_000_000, exit_horizon_us=7_000_000, fill_high=0.85, fill_low=0.65,
+                               idle_dispatch=True)
+    tuned = runtime_e2e(rtmod, rep, "resnet152", 16, 0, inflight=256, req_batch=1, workers=workers, schedule=sched,
+                        max_queue=100, slots_per_device=12, pipeline_depth=4, batching=bt)
+    tuned["config"] = "as above + idle_dispatch (MI355X tuning: no coalescing wait on an idle worker)"
+    out["mi355x_tuned"] = tuned
     del rep, m
     return out
 

@@ -72,6 +72,12 @@ typedef struct spi_batching_config {
   int32_t exit_horizon_us;     /* congestion_exit_horizon_ms */
   double fill_high, fill_low;  /* queue fill thresholds */
   double rho_high, rho_low;    /* kept for the monitor path; unused without a monitor */
+  /* This build's MI355X tuning (not in the reference): a worker with no task in flight
+   * dispatches what the queue holds at once (up to the strategy's target) instead of
+   * waiting up to coalesce_timeout_us for more jobs; batches still form from the jobs
+   * that queue while every worker is busy.  0 = the reference's collector. */
+  int32_t idle_dispatch;
+  int32_t _pad1;
 } spi_batching_config;
 
 /* BatchingStrategyRuntimeState + the `congested` flag. */

@@ -1523,7 +1523,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   // whichever slice arrives last: deterministic results.
   const int splits = a.splits;
   constexpr int SLAB = BM * BN;
-  int* words = a.p.counters + 2 * tile;  // [0] arrival ticket ([1] unused)
+  int* words = a.p.counters + tile;  // the tile's arrival ticket
   float* tile_slabs = a.p.partial + (size_t)tile * splits * SLAB;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(tile_slabs, (short)0, splits * SLAB * 4, 0x00020000);
@@ -1633,7 +1633,10 @@ struct Knobs {
   int max_split = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
   int win = 1;   // SPI_GEMM_WIN=0: 3x3/s1 tap walks without the kw window (kConvTapW)
-  int g256_min = 128;      // SPI_GEMM_256_MIN: dense F16 GEMMs with >= this many 256^2 tiles -> gemm256 (0 = off)
+  int g256_min = 128;      // SPI_GEMM_256_MIN="T256[,T128]": dense F16 GEMMs with >= T256 tiles of 256^2 -> gemm256 (0 = off)
+  // ... else with >= T128 tiles of 128 x 256 -> gemm256's 128-row tile (round 5; 0 = off)
+  int g128_min = 64;
+  int g128_nbuf = 3;  // third field: k-tile buffers of the 128-row tile (2: 96 KiB, 3: 144 KiB)
   // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
   // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
   // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
@@ -1673,7 +1676,13 @@ Knobs read_knobs() {
   }
   if (const char* e = std::getenv("SPI_GEMM_POLICY"); e && std::strncmp(e, "tput:", 5) == 0)
     k.target = std::max(1, std::atoi(e + 5));
-  if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) k.g256_min = std::atoi(e);
+  if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) {
+    int a = 0, b = 0, c = 3;
+    const int n = std::sscanf(e, "%d,%d,%d", &a, &b, &c);
+    k.g256_min = a;
+    if (n >= 2) k.g128_min = b;
+    if (n >= 3) k.g128_nbuf = c == 2 ? 2 : 3;
+  }
   if (const char* e = std::getenv("SPI_GEMM_256_LONGK"); e && *e) {
     int t = 0, kk = 0, sp = 1;
     if (std::sscanf(e, "%d,%d,%d", &t, &kk, &sp) >= 2) {
@@ -1717,17 +1726,23 @@ Knobs& knobs() {
   return k;
 }
 
-// gemm256 routing by desc (gemm() also needs 16-byte aligned A / W) and its split-K
-bool routes_256(const GemmDesc& d, Prec prec) {
+// gemm256 routing by desc (gemm() also needs 16-byte aligned A / W): the tile height it runs
+// at, 0 = the general kernel.  256^2 tiles for grids of >= T256 of them; else 128 x 256 tiles
+// for grids of >= T128 of those (BERT-base's QKV / FFN1 at bs8: 72 / 96, ViT-L's N = 1024
+// GEMMs at bs16: 100 instead of 52 256^2 tiles); else 256^2 on the long-K rule.
+int route_bm(const GemmDesc& d, Prec prec) {
   const Knobs& k = knobs();
-  return prec == Prec::F16 && (gemm256_eligible(d, prec, k.g256_min) ||
-                               (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k &&
-                                gemm256_eligible(d, prec, k.g256_longk_tiles)));
+  if (prec != Prec::F16) return 0;
+  if (gemm256_eligible(d, prec, k.g256_min)) return 256;
+  if (gemm256_eligible(d, prec, k.g128_min, 128)) return 128;
+  if (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k && gemm256_eligible(d, prec, k.g256_longk_tiles)) return 256;
+  return 0;
 }
+bool routes_256(const GemmDesc& d, Prec prec) { return route_bm(d, prec) != 0; }
 int g256_splits(const GemmDesc& d) {
   const Knobs& k = knobs();
   const int cap = k.max_split > 0 ? std::min(k.max_split, k.g256_split) : k.g256_split;
-  return cap > 1 ? gemm256_splits(d, k.target, cap) : 1;
+  return cap > 1 ? gemm256_splits(d, k.target, cap, route_bm(d, Prec::F16)) : 1;
 }
 
 Plan finish_plan(Plan pl, int ksteps, int ES, int krep = 1) {
@@ -2070,7 +2085,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
   GemmPtrs p1s = p1;
   if (q0.splits > 1) {  // keep clear of problem 0's slabs / tickets
     p1s.partial = p0.partial + (size_t)g.a[0].tiles * q0.splits * q0.bm * q0.bn;
-    p1s.counters = p0.counters + 2 * g.a[0].tiles;
+    p1s.counters = p0.counters + g.a[0].tiles;
   }
   g.a[1] = make_args<MODE>(d1, p1s, q1);
   const bool same = !q0.halo && !q1.halo && !q0.win && !q1.win && q0.bm == q1.bm && q0.bn == q1.bn &&
@@ -2092,15 +2107,17 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
 size_t gemm_partial_floats(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
   size_t f = pl.splits <= 1 ? 0 : (size_t)plan_tiles(d, pl) * pl.splits * pl.bm * pl.bn;
-  if (routes_256(d, prec) && g256_splits(d) > 1)
-    f = std::max(f, (size_t)((d.M + 255) / 256) * (d.N / 256) * g256_splits(d) * 256 * 256);
+  if (const int bm = route_bm(d, prec); bm && g256_splits(d) > 1)
+    f = std::max(f, (size_t)((d.M + bm - 1) / bm) * (d.N / 256) * g256_splits(d) * bm * 256);
   return f;
 }
 
 size_t gemm_counter_slots(const GemmDesc& d, Prec prec) {
   const Plan pl = choose_plan(d, prec);
-  size_t n = pl.splits <= 1 ? 0 : 2 * (size_t)plan_tiles(d, pl);  // per tile: arrival ticket + published-slab count
-  if (routes_256(d, prec) && g256_splits(d) > 1) n = std::max(n, 2 * (size_t)((d.M + 255) / 256) * (d.N / 256));
+  // general kernel: one arrival ticket per tile; gemm256 split-K: ticket + published-slab count
+  size_t n = pl.splits <= 1 ? 0 : (size_t)plan_tiles(d, pl);
+  if (const int bm = route_bm(d, prec); bm && g256_splits(d) > 1)
+    n = std::max(n, 2 * (size_t)((d.M + bm - 1) / bm) * (d.N / 256));
   return n;
 }
 
@@ -2200,7 +2217,7 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
     // the fold lives in the dense fp16 kernels' vector epilogue: whole 128-column tiles,
     // 16-byte aligned rows everywhere it reads or writes
     const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    const bool ok = prec == Prec::F16 && !d.conv && !d.pool_rows && d.krep == 1 && d.N % 128 == 0 &&
+    const bool ok = prec == Prec::F16 && !d.conv && !d.pool_rows && d.N % 128 == 0 &&
                     d.ldc % 8 == 0 && al16(p.C) && (!p.bias || al16(p.bias)) &&
                     (!p.res || (d.ldr % 8 == 0 && al16(p.res))) &&
                     (d.ln_in_chunks == 0 || (p.ln.in_stats && p.ln.c1 && al16(p.ln.c1))) &&
@@ -2214,7 +2231,7 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
         conv_wres(d, p, s);
       else if (routes_256(d, prec) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
                (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
-        gemm256(d, p, g256_splits(d), s);
+        gemm256(d, p, g256_splits(d), s, route_bm(d, prec), knobs().g128_nbuf);
       else
         launch<(int)Prec::F16>(d, p, s);
       break;

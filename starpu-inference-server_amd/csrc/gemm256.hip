@@ -71,23 +71,54 @@ struct G256Args {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMaxSplits = 4;     // split-K slices (gemm256_splits)
 constexpr int kMinSliceKt = 16;   // k-tiles per slice at least (ViT-L out-proj, K = 1024, 2 x 8: 52.9 us b2b vs 40.2 unsplit)
-constexpr int kBufBytes = 65536;  // one k-tile: A 256 x 128 B + B 256 x 128 B
 // diagnostic build -DSPI_G256_EPI_CALLS: leave the epilogue instances to the inliner (A/B)
 #ifdef SPI_G256_EPI_CALLS
 #define SPI_G256_EPI_INLINE
 #else
 #define SPI_G256_EPI_INLINE __attribute__((always_inline))
 #endif
-constexpr int kBOff = 32768;
 
-// 8-row piece base (tile row) of piece pc (0..15) of quarter q
+// Tile geometry by tile height BM (256: the 256 x 256 tile; 128: the 128 x 256 tile, round 5).
+//   A k-tile is BM A rows + 256 B rows of 128 bytes: 64 KiB / 48 KiB.
+//   BM = 256: two buffers, staged in 4 quarters of 16 KiB (below); BM = 128: three buffers
+//   (144 KiB), staged in 3 thirds of 16 KiB -- T0 = the 128 A rows, T1 / T2 = the B rows of
+//   n-half 0 / 1 -- one k-tile runs as 2 phases of 16 MFMAs (a wave owns 64 x 64: phase 0
+//   reads A + B n-half 0, phase 1 B n-half 1), and the third k-tile ahead is in flight.
+template <int BM, int NBUF>
+struct G256Geo {
+  static_assert(NBUF == 2 || (BM == 128 && NBUF == 3), "two k-tile buffers, three for 128-row tiles");
+  static constexpr int kBufBytes = BM * 128 + 256 * 128;
+  static constexpr int kBOff = BM * 128;
+  static constexpr int kNBuf = NBUF;
+  static constexpr int kNQ = BM == 256 ? 4 : 3;  // staging pieces of 16 KiB per k-tile
+  static constexpr int kMA = BM / 32;             // 16-row fragments per wave (wave tile BM/2 x 64)
+  static constexpr int kLds = kNBuf * kBufBytes;
+  // the epilogue parks the tile in rounds of kRoundRows x 256 fp32: one wave row's rows per round,
+  // or (128-row tile, three buffers) both wave rows at once
+  static constexpr int kRoundRows = (BM == 128 && NBUF == 3) ? 128 : BM / 2;
+  static_assert(kLds >= kRoundRows * 256 * 4, "an epilogue round parks kRoundRows x 256 fp32");
+};
+
+// 8-row piece base (tile row) of piece pc (0..15) of staging piece q
+template <int BM>
 __device__ __forceinline__ int quarter_row(int q, int pc) {
+  if constexpr (BM == 128) {
+    switch (q) {
+      case 0: return pc * 8;                           // A rows 0..127
+      case 1: return 64 * (pc >> 2) + (pc & 3) * 8;    // B n-half 0
+      default: return 64 * (pc >> 2) + 32 + (pc & 3) * 8;  // B n-half 1
+    }
+  }
   switch (q) {
     case 0: return pc < 8 ? pc * 8 : 128 + (pc - 8) * 8;
     case 1: return 64 * (pc >> 2) + (pc & 3) * 8;
     case 2: return 64 * (pc >> 2) + 32 + (pc & 3) * 8;
     default: return pc < 8 ? 64 + pc * 8 : 192 + (pc - 8) * 8;
   }
+}
+template <int BM>
+__device__ __forceinline__ constexpr bool quarter_is_a(int q) {
+  return BM == 128 ? q == 0 : (q == 0 || q == 3);
 }
 
 // RES: 0 no residual, 1 fp16 residual, 2 fp32 residual (a template parameter: the epilogue walk
@@ -124,15 +155,17 @@ __device__ __forceinline__ void bar() {
 }
 
 // Ping-pong wave rows (the lock-step two-tile-ahead variant measured C5 -2.3 % and was removed, round 4)
-template <int RES>
+template <int RES, int BM, int NBUF>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
+  using Geo = G256Geo<BM, NBUF>;
+  constexpr int kBufBytes = Geo::kBufBytes, kBOff = Geo::kBOff, kNQ = Geo::kNQ, kMA = Geo::kMA;
   // ONE LDS object: with a second __shared__ variable beside the k-tile buffers hipcc's waitcnt
   // pass could no longer tell the LDS-DMA destinations from the fragment reads and put a
   // vmcnt(0) in front of every phase's reads (ViT-L FFN1 / QKV +15 %, round 4)
-  // and exactly the two k-tile buffers: 2 KiB more (the LayerNorm statistics, round 4) made
+  // and exactly the k-tile buffers: 2 KiB more (the LayerNorm statistics, round 4) made
   // every launch 2-5 % slower (tools/ab_gemm.py, -DSPI_G256_LDS128 against it).  The split-K
   // ticket lives in buffer 0 once the k-loop's last reads are done; the statistics in registers.
-  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];
+  __shared__ __attribute__((aligned(16))) char lds[Geo::kLds];
   int* const s_ticket = reinterpret_cast<int*>(lds);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -145,22 +178,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int slice = wgid / tiles, tile = wgid - slice * tiles;
   const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * BM, n0 = tn * 256;
   const int kt0 = slice * g.ktp;
   const int KT = min(g.ktp, (g.K >> 6) - kt0);
 
-  // per-lane DMA sources of each quarter's two pieces (k-tile 0); advance 128 B per k-tile
-  const char* src[4][2];
-  int dsto[4][2];
+  // per-lane DMA sources of each staging piece's two 1 KiB parts (k-tile 0); advance 128 B per k-tile
+  const char* src[kNQ][2];
+  int dsto[kNQ][2];
   {
     const int rl = lane >> 3, chunk = (lane & 7) ^ rl;  // row within the 8-row piece, swizzled chunk
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < kNQ; ++q)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int base = quarter_row(q, wave * 2 + j);
+        const int base = quarter_row<BM>(q, wave * 2 + j);
         const int r = base + rl;
-        if (q == 0 || q == 3) {
+        if (quarter_is_a<BM>(q)) {
           const int m = min(m0 + r, g.M - 1);  // rows past M: a valid row, never stored
           src[q][j] = reinterpret_cast<const char*>(g.A + (size_t)m * g.lda + kt0 * 64) + chunk * 16;
           dsto[q][j] = base * 128;
@@ -170,8 +203,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
         }
       }
   }
+  auto bufof = [&](int kt) -> char* {
+    if constexpr (Geo::kNBuf == 2)
+      return lds + (kt & 1) * kBufBytes;
+    else
+      return lds + (kt % 3) * kBufBytes;
+  };
   auto stage = [&](int q, int kt) {
-    char* buf = lds + (kt & 1) * kBufBytes;
+    char* buf = bufof(kt);
     const int kofs = kt * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -179,13 +218,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
                                        (lds_ptr_t)(buf + dsto[q][j]), 16, 0, 0);
   };
 
-  floatx4 acc[8][4];
+  floatx4 acc[kMA][4];
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < kMA; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-  half8 fa[2][2][4];  // [m half][kk][i]
-  half8 fb[2][2][2];  // [n half][kk][j]
+  half8 fa[kMA / 4][2][4];  // [m half][kk][i]
+  half8 fb[2][2][2];        // [n half][kk][j]
 
   auto rd = [&](const char* img, int row, int c) -> half8 {
     return *reinterpret_cast<const half8*>(img + row * 128 + ((c ^ (row & 7)) << 4));
@@ -194,7 +233,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[mq][kk][i] = rd(buf, 128 * wr + 64 * mq + 16 * i + fr, kk * 4 + fq);
+      for (int i = 0; i < 4; ++i) fa[mq][kk][i] = rd(buf, (BM / 2) * wr + 64 * mq + 16 * i + fr, kk * 4 + fq);
   };
   auto read_b = [&](const char* buf, int nq) {
 #pragma unroll
@@ -215,7 +254,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  {
+  if constexpr (BM == 256) {
     // Ping-pong (cdna_hip_programming.md §5, the 256² 8-phase template): every phase is
     //   [reads of its fragments, one quarter's LDS-DMA, counted vmcnt] B_a [MFMAs] B_b
     // and wave row 1 runs one barrier behind wave row 0 (an extra s_barrier up front, one
@@ -239,7 +278,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (wr == 1) bar();  // the skew
     auto ktile = [&](int kt, auto rem_c) {
       constexpr int R = decltype(rem_c)::value;
-      const char* buf = lds + (kt & 1) * kBufBytes;
+      const char* buf = bufof(kt);
       // phase 0
       read_a(buf, 0);
       read_b(buf, 0);
@@ -272,6 +311,98 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
     ktile(KT - 1, std::integral_constant<int, 0>{});
     if (wr == 0) bar();  // the skew, closed
+  } else if constexpr (NBUF == 3) {
+    // 128 x 256: the same ping-pong of the two wave rows, 2 phases per k-tile, three buffers.
+    //   phase 0: reads A + B n-half 0 (T0, T1), stages T2 of tile t + 2, MFMAs (0, 0)
+    //   phase 1: reads B n-half 1 (T2),        stages T0 + T1 of tile t + 3, MFMAs (0, 1)
+    // The thirds go out in one sequence T0(0) T1(0) T2(0) T0(1) ... (the prologue issues the
+    // first 8); a region is restaged one phase after its last read (T2(t + 2) lands in the
+    // buffer of tile t - 1, whose T2 was read in the phase before; T0 / T1 (t + 3) in tile t's,
+    // read in phase 0), and every third has ~4 phases to land: 12 of a wave's pieces stay in
+    // flight at each wait (96 KiB per CU), never vmcnt(0) before the last k-tile.
+    // With R = KT - 1 - t tiles after tile t, the waits after each phase's DMA:
+    //   phase 0 (T2(t) must have landed):      6 min(R, 2) pieces younger
+    //   phase 1 (T0, T1(t + 1) must have):     2 (1 + 3 [R >= 2] + 2 [R >= 3]); R = 0: none
+    const int npro = min(8, 3 * KT);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < npro) stage(q % 3, q / 3);
+    if (KT >= 3)
+      vm_wait_nolgkm<12>();
+    else if (KT == 2)
+      vm_wait_nolgkm<8>();
+    else
+      vm_wait_nolgkm<2>();
+    if (wr == 1) bar();  // the skew
+    auto ktile = [&](int kt, auto rem_c) {
+      constexpr int R = decltype(rem_c)::value;
+      const char* buf = bufof(kt);
+      // phase 0
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if constexpr (R >= 2) stage(2, kt + 2);
+      vm_wait_nolgkm<6 * (R < 2 ? R : 2)>();
+      mma(0, 0);
+      bar();
+      // phase 1
+      read_b(buf, 1);
+      if constexpr (R >= 3) {
+        stage(0, kt + 3);
+        stage(1, kt + 3);
+      }
+      if constexpr (R >= 1)
+        vm_wait_nolgkm<2 * (1 + (R >= 2 ? 3 : 0) + (R >= 3 ? 2 : 0))>();
+      else
+        bar();
+      mma(0, 1);
+      bar();
+    };
+    for (int kt = 0; kt < KT - 3; ++kt) ktile(kt, std::integral_constant<int, 3>{});
+    if (KT > 2) ktile(KT - 3, std::integral_constant<int, 2>{});
+    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
+    ktile(KT - 1, std::integral_constant<int, 0>{});
+    if (wr == 0) bar();  // the skew, closed
+  } else {
+    // 128 x 256 on two buffers (96 KiB: room for another kernel's 64 KiB workgroup on the CU).
+    //   phase 0: reads T0, T1, stages T2 of tile t + 1 (its region's last read: tile t - 1, phase 1)
+    //   phase 1: reads T2,     stages T0 + T1 of tile t + 2 (read in tile t's phase 0)
+    // so a third has ~2 phases to land; waits (R = KT - 1 - t):
+    //   phase 0 (T2(t)):         6 [R >= 1] pieces younger
+    //   phase 1 (T0, T1(t + 1)): 2 (1 + 2 [R >= 2]); R = 0: none
+    const int npro = min(5, 3 * KT);
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      if (q < npro) stage(q % 3, q / 3);
+    if (KT >= 2)
+      vm_wait_nolgkm<6>();
+    else
+      vm_wait_nolgkm<2>();
+    if (wr == 1) bar();  // the skew
+    auto ktile = [&](int kt, auto rem_c) {
+      constexpr int R = decltype(rem_c)::value;
+      const char* buf = bufof(kt);
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if constexpr (R >= 1) stage(2, kt + 1);
+      vm_wait_nolgkm<R >= 1 ? 6 : 0>();
+      mma(0, 0);
+      bar();
+      read_b(buf, 1);
+      if constexpr (R >= 2) {
+        stage(0, kt + 2);
+        stage(1, kt + 2);
+      }
+      if constexpr (R >= 1)
+        vm_wait_nolgkm<2 * (1 + (R >= 2 ? 2 : 0))>();
+      else
+        bar();
+      mma(0, 1);
+      bar();
+    };
+    for (int kt = 0; kt < KT - 2; ++kt) ktile(kt, std::integral_constant<int, 2>{});
+    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
+    ktile(KT - 1, std::integral_constant<int, 0>{});
+    if (wr == 0) bar();  // the skew, closed
   }
 
   if (g.splits > 1) {
@@ -282,7 +413,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     // loads).  Partials are summed in slice order whichever slice arrives last (((p0 + p1) + p2)
     // + p3, the own partial from registers, slots past `splits` read as 0 through the buffer
     // range): results do not depend on arrival order.
-    constexpr int SLAB = 256 * 256;
+    constexpr int SLAB = BM * 256;
     int* words = g.counters + 2 * tile;
     float* slabs = g.partial + (size_t)tile * g.splits * SLAB;
     const __amdgpu_buffer_rsrc_t rs =
@@ -291,7 +422,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     __syncthreads();
     if (*s_ticket < g.splits - 1) {
 #pragma unroll
-      for (int a = 0; a < 8; ++a)
+      for (int a = 0; a < kMA; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b]), rs,
@@ -308,7 +439,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     }
     __syncthreads();
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
+    for (int a = 0; a < kMA; ++a) {
       floatx4 v[kMaxSplits][4];
 #pragma unroll
       for (int z = 0; z < kMaxSplits; ++z)
@@ -345,10 +476,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) bv[b] = g.bias ? g.bias[n0 + 64 * wc + 16 * b + fr] : 0.f;
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < kMA; ++a)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int m = m0 + 128 * wr + 16 * a + 4 * fq + v;
+        const int m = m0 + (BM / 2) * wr + 16 * a + 4 * fq + v;
         if (m >= g.M) continue;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -408,13 +539,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     constexpr bool GUARD = decltype(guard_c)::value;  // the tile crosses M
     constexpr bool LNC = decltype(lnc_c)::value;
     constexpr bool LNO = decltype(lno_c)::value;
-    [[maybe_unused]] float2 ln_st[2];
+    constexpr int kRR = Geo::kRoundRows, kRounds = BM / kRR, kPasses = kRR / 16;  // rounds of the LDS-parked tile
+    [[maybe_unused]] float2 ln_st[kRounds];
     [[maybe_unused]] float c18[8];
     if constexpr (LNC) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < kRounds; ++h) {
         float mean, rstd;
-        ln_row_stats(g.ln_in_stats, min(m0 + 128 * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks,
+        ln_row_stats(g.ln_in_stats, min(m0 + kRR * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks,
                      g.ln_in_eps, mean, rstd);
         ln_st[h] = float2{mean, rstd};
       }
@@ -427,14 +559,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kRounds; ++h) {
       // residual rows: the first half of the round's prefetched, the rest loaded inside the
       // walk (all eight would spill next to the accumulators the other wave row still holds)
       constexpr int PRE = 4;
       half8 rvh[RES == 1 ? PRE : 1];
       floatx4 rvf[RES == 2 ? PRE : 1][2];
       auto res_row = [&](int pass) -> size_t {
-        const int m = min(m0 + 128 * h + r0 + 16 * pass, g.M - 1);
+        const int m = min(m0 + kRR * h + r0 + 16 * pass, g.M - 1);
         return (size_t)m * g.ldr + nb;
       };
       if constexpr (RES == 1) {
@@ -451,14 +583,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
         }
       }
       __syncthreads();  // the k-loop's last reads / the previous round's walk are done
-      if (wr == h) {
+      // BM = 256: wave row h owns the round's 128 rows; BM = 128: both wave rows park at once
+      if (kRR == BM || wr == h) {
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
+        for (int a = 0; a < kMA; ++a)
 #pragma unroll
           for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              const int row = 16 * a + 4 * fq + v;
+              const int row = (kRR == BM ? (BM / 2) * wr : 0) + 16 * a + 4 * fq + v;
               const int col = (64 * wc + 16 * b + fr) ^ (((row >> 2) & 3) << 4);
               T[row * 256 + col] = acc[a][b][v];
             }
@@ -466,9 +599,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       __syncthreads();
       {
 #pragma unroll
-        for (int pass = 0; pass < 8; ++pass) {
+        for (int pass = 0; pass < kPasses; ++pass) {
           const int row = r0 + 16 * pass;
-          const int m = m0 + 128 * h + row;
+          const int m = m0 + kRR * h + row;
           const float* src = T + row * 256 + ((8 * cg) ^ (((row >> 2) & 3) << 4));
           const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
           const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
@@ -553,7 +686,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     }
 };
   auto by_guard = [&](auto act_c, auto f32_c, auto lnc_c, auto lno_c) SPI_G256_EPI_INLINE {
-    if (m0 + 256 <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
+    if (m0 + BM <= g.M)  // workgroup-uniform: only the last tile row takes the guarded walk
       epi(act_c, f32_c, std::false_type{}, lnc_c, lno_c);
     else
       epi(act_c, f32_c, std::true_type{}, lnc_c, lno_c);
@@ -592,8 +725,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 
 void gemm256_reload_env() {}
 
-int gemm256_splits(const GemmDesc& d, int target, int max_split) {
-  const int tiles = (d.M + 255) / 256 * (d.N / 256), kt = d.K / 64;
+int gemm256_splits(const GemmDesc& d, int target, int max_split, int bm) {
+  const int tiles = (d.M + bm - 1) / bm * (d.N / 256), kt = d.K / 64;
   if (tiles >= target || max_split == 1) return 1;
   int s = std::min({(target + tiles - 1) / tiles, kt / kMinSliceKt, kMaxSplits});
   if (max_split > 0) s = std::min(s, max_split);
@@ -602,16 +735,20 @@ int gemm256_splits(const GemmDesc& d, int target, int max_split) {
   return (kt + ktp - 1) / ktp;
 }
 
-bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles) {
+bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles, int bm) {
   if (min_tiles <= 0 || prec != Prec::F16 || d.conv || d.krep != 1 || d.a_split || d.out_split || d.pool_rows ||
       d.out_f16)
     return false;
   if (d.N % 256 || d.K % 64 || d.Kpad != d.K || d.lda % 8 || d.M < 1) return false;
-  return (d.M + 255) / 256 * (d.N / 256) >= min_tiles;
+  // no post-LN residual epilogue here (BERT's out-proj / FFN2 under the LayerNorm fold keep the
+  // general kernel at every size; gemm256() rejects them)
+  if (d.res_ln_chunks > 0) return false;
+  return (d.M + bm - 1) / bm * (d.N / 256) >= min_tiles;
 }
 
-void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
+void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm, int nbuf) {
   if (d.N % 256 || d.K % 64 || d.Kpad != d.K) throw std::invalid_argument("gemm256: N % 256, K % 64, Kpad == K");
+  if (bm != 256 && bm != 128) throw std::invalid_argument("gemm256: 256- or 128-row tiles");
   if (splits < 1 || splits > kMaxSplits || (splits > 1 && (!p.partial || !p.counters)))
     throw std::invalid_argument("gemm256: 1..4 split-K slices, with slabs and counters");
   G256Args g;
@@ -627,7 +764,7 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
   g.M = d.M;
   g.N = d.N;
   g.K = d.K;
-  g.tiles_m = (d.M + 255) / 256;
+  g.tiles_m = (d.M + bm - 1) / bm;
   g.tiles_n = d.N / 256;
   g.act = static_cast<int>(d.act);
   g.res_f32 = d.res_f32;
@@ -658,12 +795,28 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s) {
   g.counters = p.counters;
   const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
   const dim3 grid(g.tiles_m * g.tiles_n * g.splits), blk(512);
-  if (res == 0)
-    SPI_LAUNCH((gemm256_kernel<0>), grid, blk, 0, s, g);
-  else if (res == 1)
-    SPI_LAUNCH((gemm256_kernel<1>), grid, blk, 0, s, g);
-  else
-    SPI_LAUNCH((gemm256_kernel<2>), grid, blk, 0, s, g);
+  if (bm == 256) {
+    if (res == 0)
+      SPI_LAUNCH((gemm256_kernel<0, 256, 2>), grid, blk, 0, s, g);
+    else if (res == 1)
+      SPI_LAUNCH((gemm256_kernel<1, 256, 2>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<2, 256, 2>), grid, blk, 0, s, g);
+  } else if (nbuf == 3) {
+    if (res == 0)
+      SPI_LAUNCH((gemm256_kernel<0, 128, 3>), grid, blk, 0, s, g);
+    else if (res == 1)
+      SPI_LAUNCH((gemm256_kernel<1, 128, 3>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<2, 128, 3>), grid, blk, 0, s, g);
+  } else {
+    if (res == 0)
+      SPI_LAUNCH((gemm256_kernel<0, 128, 2>), grid, blk, 0, s, g);
+    else if (res == 1)
+      SPI_LAUNCH((gemm256_kernel<1, 128, 2>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<2, 128, 2>), grid, blk, 0, s, g);
+  }
 }
 
 }  // namespace spi

@@ -249,8 +249,9 @@ LinearW pack_linear_named(const PMap& p, const std::string& name, Prec prec, boo
 // the fold (ln_fold.hpp): W' = W diag(gamma) in the compute type, bias' = b + W beta, and
 // c1[n] = sum_k W'[n][k] over the packed (rounded) values, so the epilogue's
 // rstd (x W'^T - mean c1) cancels exactly what the MFMAs accumulated.
+// hilo (transformer F16M): W' packed hi + lo (krep = 2); c1 sums both halves as packed.
 LinearW pack_linear_folded(const float* w, const float* b, int N, int K, Prec prec, const float* gamma,
-                           const float* beta) {
+                           const float* beta, bool hilo = false) {
   std::vector<float> wf((size_t)N * K), bf(N);
   std::vector<float> c1(N);
   for (int n = 0; n < N; ++n) {
@@ -260,12 +261,17 @@ LinearW pack_linear_folded(const float* w, const float* b, int N, int K, Prec pr
       const float f = v * gamma[k];
       wf[(size_t)n * K + k] = f;
       bb += (double)beta[k] * v;
-      cc += prec == Prec::F16 ? (double)static_cast<float>(static_cast<_Float16>(f)) : (double)f;
+      if (prec == Prec::F16) {
+        const float hi = static_cast<float>(static_cast<_Float16>(f));
+        cc += hilo ? (double)hi + (double)static_cast<float>(static_cast<_Float16>(f - hi)) : (double)hi;
+      } else {
+        cc += (double)f;
+      }
     }
     bf[n] = (float)bb;
     c1[n] = (float)cc;
   }
-  LinearW L = pack_linear(wf.data(), bf.data(), N, K, prec);
+  LinearW L = pack_linear(wf.data(), bf.data(), N, K, prec, hilo);
   L.c1 = pack_vec(c1.data(), N);
   return L;
 }
@@ -366,6 +372,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     for (size_t i = 0; i < stage_blocks_.size(); ++i) os << (i ? "," : "") << stage_blocks_[i];
     os << "] img" << image_ << " classes" << classes_;
   } else if (family_ == SPI_FAMILY_BERT) {
+    mixed_ = cfg.precision == SPI_PREC_F16M;  // hi + lo weights on every encoder GEMM
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-12f;
     ln_fold_ = ln_fold_enabled(prec_, kBertLnFold);
     heads_ = cfg.num_heads;
@@ -373,6 +380,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     build_bert(strip_prefix(p, "embeddings.word_embeddings.weight"));
     os << "bert L" << layers_ << " D" << D_ << " H" << heads_ << " FF" << ffn_ << " S<=" << seq_;
   } else if (family_ == SPI_FAMILY_VIT) {
+    mixed_ = cfg.precision == SPI_PREC_F16M;
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-6f;
     ln_fold_ = ln_fold_enabled(prec_, kVitLnFold);
     heads_ = cfg.num_heads;
@@ -528,11 +536,11 @@ void Model::build_bert(const PMap& p) {
       std::memcpy(w.data() + (size_t)j * D_ * D_, fdata(need(p, nm + ".weight")), sizeof(float) * D_ * D_);
       std::memcpy(b.data() + (size_t)j * D_, fdata(need(p, nm + ".bias")), sizeof(float) * D_);
     }
-    L.qkv = pack_linear(w.data(), b.data(), 3 * D_, D_, prec_);
-    L.out = pack_linear_named(p, pre + "attention.output.dense", prec_);
+    L.qkv = pack_linear(w.data(), b.data(), 3 * D_, D_, prec_, mixed_);
+    L.out = pack_linear_named(p, pre + "attention.output.dense", prec_, mixed_);
     L.ln1 = pack_ln(p, pre + "attention.output.LayerNorm");
-    L.ff1 = pack_linear_named(p, pre + "intermediate.dense", prec_);
-    L.ff2 = pack_linear_named(p, pre + "output.dense", prec_);
+    L.ff1 = pack_linear_named(p, pre + "intermediate.dense", prec_, mixed_);
+    L.ff2 = pack_linear_named(p, pre + "output.dense", prec_, mixed_);
     L.ln2 = pack_ln(p, pre + "output.LayerNorm");
     ffn_ = L.ff1.n;
     tf_.push_back(L);
@@ -545,7 +553,7 @@ void Model::build_bert(const PMap& p) {
       const std::string ln1 = pre + "attention.output.LayerNorm";
       const spi_named_tensor* f1 = need(p, pre + "intermediate.dense.weight");
       tf_[i].ff1 = pack_linear_folded(fdata(f1), fdata(need(p, pre + "intermediate.dense.bias")), ffn_, D_, prec_,
-                                      fdata(need(p, ln1 + ".weight")), fdata(need(p, ln1 + ".bias")));
+                                      fdata(need(p, ln1 + ".weight")), fdata(need(p, ln1 + ".bias")), mixed_);
       if (i == 0) continue;
       const std::string ln2 = "encoder.layer." + std::to_string(i - 1) + ".output.LayerNorm";
       std::vector<float> w((size_t)3 * D_ * D_), b((size_t)3 * D_);
@@ -556,7 +564,7 @@ void Model::build_bert(const PMap& p) {
         std::memcpy(b.data() + (size_t)j * D_, fdata(need(p, nm + ".bias")), sizeof(float) * D_);
       }
       tf_[i].qkv = pack_linear_folded(w.data(), b.data(), 3 * D_, D_, prec_, fdata(need(p, ln2 + ".weight")),
-                                      fdata(need(p, ln2 + ".bias")));
+                                      fdata(need(p, ln2 + ".bias")), mixed_);
     }
   }
 }
@@ -573,7 +581,7 @@ void Model::build_vit(const PMap& p) {
   if (D_ % 64 != 0 || D_ > 1024) throw std::runtime_error("hidden size must be a multiple of 64, <= 1024");
   const int K = 3 * patch_ * patch_;
   patch_proj_ = pack_linear(fdata(cw), has(p, "conv_proj.bias") ? fdata(need(p, "conv_proj.bias")) : nullptr,
-                            D_, K, prec_);
+                            D_, K, prec_, mixed_);
   cls_ = pack_vec(fdata(need(p, "class_token")), D_);
   const spi_named_tensor* pe = need(p, "encoder.pos_embedding");
   if (numel(pe) != (int64_t)(npatch_ + 1) * D_) throw std::runtime_error("pos_embedding does not match image/patch size");
@@ -586,13 +594,13 @@ void Model::build_vit(const PMap& p) {
     L.ln1 = pack_ln(p, pre + "ln_1");
     const spi_named_tensor* iw = need(p, pre + "self_attention.in_proj_weight");
     L.qkv = pack_linear(fdata(iw), fdata(need(p, pre + "self_attention.in_proj_bias")), (int)iw->shape[0],
-                        (int)iw->shape[1], prec_);
-    L.out = pack_linear_named(p, pre + "self_attention.out_proj", prec_);
+                        (int)iw->shape[1], prec_, mixed_);
+    L.out = pack_linear_named(p, pre + "self_attention.out_proj", prec_, mixed_);
     L.ln2 = pack_ln(p, pre + "ln_2");
     const std::string m1 = has(p, pre + "mlp.0.weight") ? pre + "mlp.0" : pre + "mlp.linear_1";
     const std::string m2 = has(p, pre + "mlp.3.weight") ? pre + "mlp.3" : pre + "mlp.linear_2";
-    L.ff1 = pack_linear_named(p, m1, prec_);
-    L.ff2 = pack_linear_named(p, m2, prec_);
+    L.ff1 = pack_linear_named(p, m1, prec_, mixed_);
+    L.ff2 = pack_linear_named(p, m2, prec_, mixed_);
     ffn_ = L.ff1.n;
     tf_.push_back(L);
   }
@@ -605,16 +613,17 @@ void Model::build_vit(const PMap& p) {
       const std::string m1 = has(p, pre + "mlp.0.weight") ? pre + "mlp.0" : pre + "mlp.linear_1";
       const spi_named_tensor* f1 = need(p, m1 + ".weight");
       tf_[i].ff1 = pack_linear_folded(fdata(f1), fdata(need(p, m1 + ".bias")), (int)f1->shape[0], (int)f1->shape[1],
-                                      prec_, fdata(need(p, pre + "ln_2.weight")), fdata(need(p, pre + "ln_2.bias")));
+                                      prec_, fdata(need(p, pre + "ln_2.weight")), fdata(need(p, pre + "ln_2.bias")),
+                                      mixed_);
       if (i == 0) continue;
       const spi_named_tensor* iw = need(p, pre + "self_attention.in_proj_weight");
       tf_[i].qkv = pack_linear_folded(fdata(iw), fdata(need(p, pre + "self_attention.in_proj_bias")),
                                       (int)iw->shape[0], (int)iw->shape[1], prec_, fdata(need(p, pre + "ln_1.weight")),
-                                      fdata(need(p, pre + "ln_1.bias")));
+                                      fdata(need(p, pre + "ln_1.bias")), mixed_);
     }
   }
   final_ln_ = pack_ln(p, "encoder.ln");
-  head_ = pack_linear_named(p, "heads.head", prec_);
+  head_ = pack_linear_named(p, "heads.head", prec_, mixed_);
   classes_ = head_.n;
   seq_ = npatch_ + 1;
 }

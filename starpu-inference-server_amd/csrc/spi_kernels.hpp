@@ -131,15 +131,15 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s);
 void gemm_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, const GemmPtrs& p1, Prec prec,
                hipStream_t s);
 
-// 256x256-tile 8-wave fp16 GEMM (gemm256.hip) for large dense F16 contractions;
-// gemm() routes a desc to it when gemm256_eligible (N % 256 == 0, K % 64 == 0,
-// at least min_tiles 256^2 tiles; SPI_GEMM_256_MIN, default 128, 0 = never).
-bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles);
+// 8-wave phased fp16 GEMM (gemm256.hip), tiles of bm x 256 (bm = 256 or 128) for the dense
+// F16 contractions; gemm() routes a desc to it when gemm256_eligible (N % 256 == 0,
+// K % 64 == 0, at least min_tiles tiles of bm x 256; routing rule in gemm.hip).
+bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles, int bm = 256);
 // Split-K slices for a gemm256 problem: 1 with >= target tiles, else enough slices of >= 16
 // k-tiles (at most 4, at most max_split when > 0) to reach ~target workgroups (ViT-L's
 // N = 1024 GEMMs: 52 tiles -> FFN2 3 slices, out-proj none).
-int gemm256_splits(const GemmDesc& d, int target, int max_split);
-void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s);
+int gemm256_splits(const GemmDesc& d, int target, int max_split, int bm = 256);
+void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm = 256, int nbuf = 2);
 void gemm256_reload_env();  // no knobs left (kept for spi_debug_gemm_reload_env)
 
 // Weight-resident 3x3/s1/p1 conv, 64 -> 64 channels, fp16 NHWC (conv_wres.hip): the

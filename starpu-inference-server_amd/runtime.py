@@ -35,7 +35,7 @@ class BatchingConfig(C.Structure):
                 ("coalesce_timeout_us", C.c_int32), ("congestion_enabled", C.c_int32),
                 ("tick_interval_us", C.c_int32), ("entry_horizon_us", C.c_int32), ("exit_horizon_us", C.c_int32),
                 ("fill_high", C.c_double), ("fill_low", C.c_double), ("rho_high", C.c_double),
-                ("rho_low", C.c_double)]
+                ("rho_low", C.c_double), ("idle_dispatch", C.c_int32), ("_pad1", C.c_int32)]
 
 
 class BatchingPressure(C.Structure):
@@ -155,9 +155,11 @@ class Completion:
 def batching_config(kind: str = "fixed", min_batch: int = 1, batch_limit: int = 0, coalesce_timeout_us: int = 0,
                     congestion: bool = False, tick_us: int = 500, entry_horizon_us: int = 3000,
                     exit_horizon_us: int = 7000, fill_high: float = 0.85, fill_low: float = 0.65,
-                    rho_high: float = 1.10, rho_low: float = 0.90) -> BatchingConfig:
+                    rho_high: float = 1.10, rho_low: float = 0.90, idle_dispatch: bool = False) -> BatchingConfig:
     """Defaults follow the reference's perf config (ci/perf/resnet152_ci_perf.yml: fill 0.85/0.65,
-    rho 1.10/0.90, entry/exit horizons 3000/7000 with a 500 tick), in microseconds."""
+    rho 1.10/0.90, entry/exit horizons 3000/7000 with a 500 tick), in microseconds.
+    idle_dispatch: this build's MI355X tuning -- an idle worker dispatches the queue at once
+    instead of waiting out the coalesce timeout (include/spi_runtime.h)."""
     b = BatchingConfig()
     b.kind = BATCHING[kind]
     b.min_batch_limit = min_batch
@@ -166,6 +168,7 @@ def batching_config(kind: str = "fixed", min_batch: int = 1, batch_limit: int = 
     b.congestion_enabled = int(congestion)
     b.tick_interval_us, b.entry_horizon_us, b.exit_horizon_us = tick_us, entry_horizon_us, exit_horizon_us
     b.fill_high, b.fill_low, b.rho_high, b.rho_low = fill_high, fill_low, rho_high, rho_low
+    b.idle_dispatch = int(idle_dispatch)
     return b
 
 

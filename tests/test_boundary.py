@@ -254,10 +254,11 @@ def test_host_replica_recognition_and_flops(spi, zoo, name, kw, gflop):
     r16x3 = spi.ModelReplica(m, -1, "fp16x3", max_batch=2, **kw)
     assert "f16x3" in r16x3.description
     r16m = spi.ModelReplica(m, -1, "fp16m", max_batch=2, **kw)
-    # the mixed mode exists for the ResNets (BERT / ViT run it as plain fp16)
-    assert ("f16m" in r16m.description) == name.startswith("resnet")
+    assert "f16m" in r16m.description
     if name.startswith("resnet"):  # + the downsample lo halves, stem / FC in split fp16
         assert r.weight_bytes < r16m.weight_bytes < r16x3.weight_bytes
+    else:  # transformers: hi + lo halves of every GEMM weight (the fp32 embeddings / LN as fp16)
+        assert r16m.weight_bytes > r.weight_bytes
 
 
 def test_flops_match_torch_flop_counter(spi, zoo):

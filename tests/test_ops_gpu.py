@@ -355,23 +355,25 @@ def test_stem_pool_fused(ops, prec, B, H, W, rows):
     assert err < tol, f"stem_pool {prec} {B}x{H}x{W}: {err:.3e}"
 
 
-@pytest.fixture
-def gemm256_everywhere(ops):
+@pytest.fixture(params=["1", "0,1,3", "0,1,2"], ids=["bm256", "bm128", "bm128b2"])
+def gemm256_everywhere(ops, request):
+    """Every eligible fp16 GEMM on gemm256.hip, at tile height 256 (SPI_GEMM_256_MIN=1) or 128
+    (the 128 x 256 tile's two-phase loop on three k-tile buffers, =0,1,3, or two, =0,1,2)."""
     import os
-    os.environ["SPI_GEMM_256_MIN"] = "1"
+    os.environ["SPI_GEMM_256_MIN"] = request.param
     ops.lib.spi_debug_gemm_reload_env()
-    yield
+    yield request.param
     os.environ.pop("SPI_GEMM_256_MIN", None)
     ops.lib.spi_debug_gemm_reload_env()
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 256, 64), (300, 512, 128), (256, 768, 192), (1000, 1024, 640),
-                                   (3152, 1024, 4096)])
+                                   (3152, 1024, 4096), (1024, 2304, 768), (129, 256, 320)])
 @pytest.mark.parametrize("act,res,out_f32", [(None, None, True), ("gelu", None, False), ("relu", "f16", False),
                                              (None, "f32", True)])
 def test_gemm256_tiles(ops, gemm256_everywhere, M, N, K, act, res, out_f32):
-    """The 256x256 8-wave phased GEMM (gemm256.hip; SPI_GEMM_256_MIN=1 routes every eligible
-    fp16 GEMM to it): one k-tile (the peeled last tile only), ragged M, bias / GELU / ReLU,
+    """The 8-wave phased GEMM (gemm256.hip) at both tile heights: one k-tile (the peeled last
+    tile only), 2 to 5 k-tiles (every tail of the 128-row loop), ragged M, bias / GELU / ReLU,
     fp16 and fp32 residuals, fp16 and fp32 outputs."""
     g = torch.Generator().manual_seed(M * 3 + N + K)
     A = torch.randn(M, K, generator=g).half()

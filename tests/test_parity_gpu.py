@@ -15,7 +15,7 @@ from oracle.cpu_codelet import cpu_inference, normalized_max_error, top1_agreeme
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": 1e-5, "fp16": 1e-3, "fp16x3": 1e-5}  # fp16x3 measures 1.6e-6 .. 3.2e-6 (fp32-grade)
+TOL = {"fp32": 1e-5, "fp16": 1e-3, "fp16x3": 1e-5, "fp16m": 1e-3}  # fp16x3 measures 1.6e-6 .. 3.2e-6 (fp32-grade)
 # Plain fp16 operands on the random-init ResNets: rounding the MFMA operands
 # alone gives ~1.7e-3 normalised max error (CPU emulation: fp16 weights 1.4e-3,
 # fp16 activations 1.2e-3, both 1.67e-3 at ResNet-18 bs8@224).  That is the
@@ -134,7 +134,7 @@ def test_bert_two_layers_masked(spi, zoo, gpu, prec):
     assert err < TOL[prec]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16m"])
 def test_bert_base_seq128_bs8(spi, zoo, gpu, prec):
     """C3: bert-base-uncased seq=128 bs=8 (mask all ones)."""
     rng = np.random.default_rng(4)
@@ -162,16 +162,21 @@ def test_vit_small_seq197(spi, zoo, gpu, prec):
     assert err < TOL[prec]
 
 
+@pytest.mark.parametrize("prec", ["fp16", "fp16m"])
 @pytest.mark.parametrize("family", ["bert", "vit"])
-def test_transformer_layernorm_fold(spi, zoo, gpu, family, monkeypatch):
+def test_transformer_layernorm_fold(spi, zoo, gpu, family, prec, monkeypatch):
     """The LayerNorm fold (ln_fold.hpp, DESIGN.md 3.6: statistics from the producing GEMM's
     epilogue, gain folded into the consuming GEMM's weights, post-LN residuals recomputed
     element-wise) against the separate LayerNorm launches (SPI_LN_FOLD=0) and the oracle; the
     folded forward runs at most two LayerNorm launches.  The weights here are drawn wider than
-    HF's init (std 0.05, larger activations and row means: the fold's cancellation case), which
-    puts the unfused fp16 BERT path itself at 1.08e-3 from the oracle: the bar is that the fold
-    is no less accurate than the launches it replaces (within 10 %) and within 1.5e-3 -- the
-    1e-3 bars of the BASELINE configs are test_bert_base_seq128_bs8 / the full-size tests."""
+    HF's init (std 0.05, larger activations and row means: the fold's cancellation case).
+    fp16m (hi + lo weights on every GEMM) holds both paths under the 1e-3 bar.  Plain fp16 sits
+    at the bar on this model: the CPU emulation of the fp16 path (tools/prec_emulate_bert.py)
+    puts the unfused path at 1.00e-3 and the folded one at 1.04e-3, spread over every rounding
+    site (weights 0.35e-3 of it, no other site more than 0.1e-3), so its bar is
+    that the fold is no less accurate than the launches it replaces (within 10 %) and within
+    1.5e-3 -- the 1e-3 bars of the BASELINE configs are test_bert_base_seq128_bs8 / the full-size
+    tests."""
     rng = np.random.default_rng(13)
     if family == "bert":
         m = zoo.bert(layers=3, init_std=0.05)
@@ -182,19 +187,55 @@ def test_transformer_layernorm_fold(spi, zoo, gpu, family, monkeypatch):
         inputs, kw = [image(rng, 2, 224)], dict(max_batch=2)
     ref = cpu_inference(m, inputs)[0]
     monkeypatch.setenv("SPI_LN_FOLD", "1")  # whatever the family's default
-    rep = spi.ModelReplica(m, 0, "fp16", **kw)
+    rep = spi.ModelReplica(m, 0, prec, **kw)
     folded = hip_forward(spi, rep, inputs, ref.shape, graphs=True)
     ins = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in inputs]
     out = torch.empty(ref.shape, device="cuda")
     ops = rep.profile(ins, out, torch.cuda.current_stream().cuda_stream)
     n_ln = sum(1 for o in ops if o["name"].startswith("layernorm"))
     monkeypatch.setenv("SPI_LN_FOLD", "0")
-    plain = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), inputs, ref.shape)
+    plain = hip_forward(spi, spi.ModelReplica(m, 0, prec, **kw), inputs, ref.shape)
     d = normalized_max_error(folded, plain)
     e_f, e_p = normalized_max_error(folded, ref), normalized_max_error(plain, ref)
-    print(f"{family} LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e}), LN launches {n_ln}")
+    print(f"{family} {prec} LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e}), LN launches {n_ln}")
     assert n_ln <= 2
-    assert e_f < 1.5e-3 and e_f <= 1.1 * e_p, (e_f, e_p, d)
+    if prec == "fp16m":
+        assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3, (e_f, e_p, d)
+    else:
+        assert e_f < 1.5e-3 and e_f <= 1.1 * e_p, (e_f, e_p, d)
+
+
+@pytest.mark.parametrize("family", ["vit", "bert"])
+@pytest.mark.parametrize("route", ["0,1,3", "0,1,2", "1"], ids=["bm128", "bm128b2", "bm256"])
+def test_transformer_layernorm_fold_on_gemm256(spi, zoo, gpu, family, route, monkeypatch):
+    """The LayerNorm fold's gemm256 epilogues (consumer statistics + c1 on QKV / FFN1, producer
+    chunk statistics + fp16 copy on ViT's out-proj / FFN2; BERT's post-LN producers stay on the
+    general kernel) at width 256, every eligible GEMM forced onto gemm256 at tile height 128
+    (SPI_GEMM_256_MIN=0,1) or 256 (=1), 394 / 240 token rows (ragged last tile row): folded
+    vs the separate LayerNorm launches on the same kernels, and both vs the oracle."""
+    rng = np.random.default_rng(29)
+    if family == "bert":
+        m = zoo.bert(layers=2, hidden=256, heads=4, intermediate=1024)
+        ids, mask = bert_inputs(rng, 3, 80, pad_from=50)
+        inputs, kw = [ids, mask], dict(max_batch=3, seq_len=128)
+    else:
+        m = zoo.vit(image=224, patch=16, layers=2, heads=4, dim=256, mlp_dim=512)
+        inputs, kw = [image(rng, 2, 224)], dict(max_batch=2)
+    ref = cpu_inference(m, inputs)[0]
+    monkeypatch.setenv("SPI_GEMM_256_MIN", route)
+    monkeypatch.setenv("SPI_LN_FOLD", "1")
+    spi.lib.spi_debug_gemm_reload_env()
+    try:
+        folded = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), inputs, ref.shape)
+        monkeypatch.setenv("SPI_LN_FOLD", "0")
+        plain = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), inputs, ref.shape)
+    finally:
+        monkeypatch.delenv("SPI_GEMM_256_MIN")
+        spi.lib.spi_debug_gemm_reload_env()
+    d = normalized_max_error(folded, plain)
+    e_f, e_p = normalized_max_error(folded, ref), normalized_max_error(plain, ref)
+    print(f"{family} gemm256 {route} LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e})")
+    assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3, (e_f, e_p, d)
 
 
 def test_affine_codelet_like_reference(spi, gpu):

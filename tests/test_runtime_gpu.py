@@ -257,13 +257,16 @@ def test_runtime_fixed_worker_and_priority(spi, zoo, rtmod):
     rt.close()
 
 
-def test_runtime_adaptive_batching_under_load(spi, zoo, rtmod):
+@pytest.mark.parametrize("idle_dispatch", [False, True])
+def test_runtime_adaptive_batching_under_load(spi, zoo, rtmod, idle_dispatch):
     """AdaptiveBatchingStrategy in the runtime: bs1 requests under a backlog grow the target
-    (queue fill / in-flight pressure) and every merged job still gets its own rows back."""
+    (queue fill / in-flight pressure) and every merged job still gets its own rows back --
+    also with idle_dispatch (no coalescing wait on an idle worker: batches form from the
+    backlog alone)."""
     m = zoo.resnet18(image=64)
     rep = spi.ModelReplica(m, 0, "fp16x3", max_batch=8, image_size=64)
     b = rtmod.batching_config("adaptive", min_batch=1, batch_limit=8, coalesce_timeout_us=200, congestion=True,
-                              tick_us=100, entry_horizon_us=400, exit_horizon_us=2000)
+                              tick_us=100, entry_horizon_us=400, exit_horizon_us=2000, idle_dispatch=idle_dispatch)
     rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8, workers_per_device=2,
                        max_queue=64, batching=b)
     rng = np.random.default_rng(12)
@@ -278,6 +281,26 @@ def test_runtime_adaptive_batching_under_load(spi, zoo, rtmod):
     assert max(c.task_batch for c in rt.completions) > 1
     assert 1 <= rt.batch_target <= 8
     rt.close()
+
+
+def test_runtime_idle_dispatch_skips_the_coalescer(spi, zoo, rtmod):
+    """idle_dispatch on a sparse open-loop schedule (one request every 2 ms, a 20 ms coalesce
+    timeout): the reference's collector holds each request for the timeout while the GPU idles;
+    with idle_dispatch the idle worker runs it at once, so p50 falls far below the timeout."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16", max_batch=8, image_size=64, graphs=True)
+    x = np.random.default_rng(14).random((1, 3, 64, 64), dtype=np.float32)
+    p50 = {}
+    for idle in (False, True):
+        b = rtmod.batching_config("adaptive", 1, 8, coalesce_timeout_us=20_000, idle_dispatch=idle)
+        rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8,
+                           workers_per_device=2, max_queue=64, batching=b)
+        r = rt.loadgen([x], schedule=[(2000, 40)])
+        assert r["completed"] == 40 and r["failed"] == 0
+        p50[idle] = r["p50_ms"]
+        rt.close()
+    print(f"p50 coalescer {p50[False]:.2f} ms, idle dispatch {p50[True]:.2f} ms")
+    assert p50[True] < 5.0 < p50[False]
 
 
 def test_runtime_loadgen_closed_and_open_loop(spi, zoo, rtmod):
