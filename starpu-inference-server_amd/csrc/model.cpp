@@ -373,6 +373,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     os << "] img" << image_ << " classes" << classes_;
   } else if (family_ == SPI_FAMILY_BERT) {
     mixed_ = cfg.precision == SPI_PREC_F16M;  // hi + lo weights on every encoder GEMM
+    if (const char* e = std::getenv("SPI_QKV_ATTN"); e && *e) qkv_fused_ = std::atoi(e) != 0;
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-12f;
     ln_fold_ = ln_fold_enabled(prec_, kBertLnFold);
     heads_ = cfg.num_heads;
@@ -891,6 +892,31 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   if (prof_) op_end(s);
 }
 
+void Model::run_qkv_attention(const LinearW& L, const void* x, const float* in_stats, void* qkv, void* ctx, int B,
+                              int S, Workspace& w, hipStream_t s) {
+  const int T = B * S, hd = D_ / heads_;
+  const float scale = 1.0f / std::sqrt((float)hd);
+  const float* mask = w.has_mask ? w.mask_bias : nullptr;
+  if (qkv_fused_ && f16_ && L.prec == Prec::F16 &&
+      qkv_attention_eligible(S, heads_, hd, L.k, L.kpad, L.krep, D_, L.kpad) && (!in_stats || L.c1)) {
+    const int nrep = !prof_ ? 1 : op_begin(s, "qkv_attention_S" + std::to_string(S),
+                                           2.0 * T * L.n * (double)L.k + 4.0 * B * S * S * D_,
+                                           (double)T * D_ * 2 * 2 + (double)L.n * L.k * 2);
+    for (int r = 0; r < nrep; ++r)
+      qkv_attention(x, D_, ptr<void>(L.w), L.kpad, ptr<float>(L.b), in_stats, in_stats ? ptr<float>(L.c1) : nullptr,
+                    D_ / 64, eps_, mask, ctx, B, S, heads_, scale, s);
+    if (prof_) op_end(s);
+    return;
+  }
+  LnSpec q;
+  q.in_stats = const_cast<float*>(in_stats);
+  run_gemm(L, x, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s, in_stats ? &q : nullptr);
+  const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
+                                         (double)T * 4 * D_ * (f16_ ? 2 : 4));
+  for (int r = 0; r < nrep; ++r) attention(qkv, mask, ctx, B, S, heads_, hd, scale, f16_, s);
+  if (prof_) op_end(s);
+}
+
 // avgpool + fc as one GEMM over every pixel of the last stage with a
 // column-mean epilogue (GemmDesc::pool_rows): the split / fp16 / fp32 activation
 // is the A operand as is, so the pooled vector never goes through HBM.
@@ -1135,7 +1161,6 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     void* ctx = w.bufs[3];
     float* a = static_cast<float*>(w.bufs[4]);
     void* ff = w.bufs[5];
-    const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     if (ln_fold_) {
       // Post-LN with the LayerNorms folded (ln_fold.hpp): hf holds the embedding output, then
       // each layer's pre-LN2 rows b; a the pre-LN1 rows; ht the fp16 copy the next GEMM reads;
@@ -1149,14 +1174,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       float* S2 = static_cast<float*>(w.bufs[7]);
       for (int i = 0; i < layers_; ++i) {
         const TfLayer& L = tf_[i];
-        LnSpec q;
-        if (i > 0) q.in_stats = S2;
-        run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
-        const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
-                                               (double)T * 4 * D_ * 2);
-        for (int r = 0; r < nrep; ++r)
-          attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
-        if (prof_) op_end(s);
+        run_qkv_attention(L.qkv, ht, i > 0 ? S2 : nullptr, qkv, ctx, B, S, w, s);
         LnSpec o;
         if (i > 0) {
           o.res_stats = S2;
@@ -1181,12 +1199,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     }
     for (int i = 0; i < layers_; ++i) {
       const TfLayer& L = tf_[i];
-      run_gemm(L.qkv, ht, T, D_, qkv, 3 * D_, false, Act::None, nullptr, false, 0, w, s);
-      const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
-                                             (double)T * 4 * D_ * (f16_ ? 2 : 4));
-      for (int r = 0; r < nrep; ++r)
-        attention(qkv, w.has_mask ? w.mask_bias : nullptr, ctx, B, S, heads_, D_ / heads_, scale, f16_, s);
-      if (prof_) op_end(s);
+      run_qkv_attention(L.qkv, ht, nullptr, qkv, ctx, B, S, w, s);
       run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s);
       prof_op(s, "layernorm", ln_bytes(T, true), [&] {
         layernorm(a, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), hf, f16_ ? ht : nullptr, D_, T, D_, eps_, f16_, s);

@@ -125,6 +125,10 @@ class Model {
   void run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc,
                 bool out_f32, Act act, const void* res, bool res_f32, int ldr, Workspace& ws,
                 hipStream_t s, const LnSpec* ln = nullptr);
+  // QKV projection + attention of one transformer layer: the fused kernel (qkv_attn.hip) when
+  // the shape allows it, else the QKV GEMM into qkv and the attention launch
+  void run_qkv_attention(const LinearW& L, const void* x, const float* in_stats, void* qkv, void* ctx, int B,
+                         int S, Workspace& ws, hipStream_t s);
   void run_conv(const ConvW& c, const void* x, int B, int H, int W, void* y, int& OH, int& OW,
                 Act act, const void* res, Workspace& ws, hipStream_t s, bool out_f32 = false,
                 bool res_f32 = false);
@@ -182,6 +186,7 @@ class Model {
   // LayerNorm folded across the GEMMs (fp16, D and FFN multiples of 128; SPI_LN_FOLD=0: the
   // separate LayerNorm launches): no LN launch inside the encoder stack
   bool ln_fold_ = false;
+  bool qkv_fused_ = true;  // SPI_QKV_ATTN=0: the QKV GEMM + attention launches (A/B)
   size_t word_ = 0, pos_ = 0, type0_ = 0;
   LnW emb_ln_, final_ln_;
   std::vector<TfLayer> tf_;

@@ -142,6 +142,15 @@ int gemm256_splits(const GemmDesc& d, int target, int max_split, int bm = 256);
 void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm = 256, int nbuf = 2);
 void gemm256_reload_env();  // no knobs left (kept for spi_debug_gemm_reload_env)
 
+// Fused QKV projection + attention for S <= 128 (qkv_attn.hip): one workgroup per (sequence,
+// head) runs the head's q | k | v GEMM (A rows lda apart, packed W rows ldw apart; with
+// ln_stats: the LayerNorm consumer fold, ln_fold.hpp) and the attention on the LDS-resident
+// result, writing ctx [B S][heads 64] fp16.
+bool qkv_attention_eligible(int S, int heads, int hd, int K, int kpad, int krep, int lda, int ldw);
+void qkv_attention(const void* A, int lda, const void* W, int ldw, const float* bias, const float* ln_stats,
+                   const float* c1, int ln_chunks, float ln_eps, const float* mask_bias, void* ctx, int B, int S,
+                   int heads, float scale, hipStream_t s);
+
 // Weight-resident 3x3/s1/p1 conv, 64 -> 64 channels, fp16 NHWC (conv_wres.hip): the
 // folded weights stay in LDS while a workgroup walks bands of output rows; gemm()
 // routes an eligible desc to it (SPI_CONV_WRES=0: never).

@@ -238,6 +238,29 @@ def test_transformer_layernorm_fold_on_gemm256(spi, zoo, gpu, family, route, mon
     assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3, (e_f, e_p, d)
 
 
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("S,pad_from", [(128, None), (80, 50), (16, 9), (128, 100)])
+def test_bert_qkv_attention_fused(spi, zoo, gpu, S, pad_from, fold, monkeypatch):
+    """The fused QKV projection + attention kernel (qkv_attn.hip: one workgroup per (sequence,
+    head), the head's q | k | v GEMM, then the attention on the LDS-resident Q / K / V) against
+    the QKV GEMM + attention launches it replaces (SPI_QKV_ATTN=0) and the oracle: full and
+    ragged sequences (S < 128: rows past S clamped and zeroed), padding masks, with and without
+    the LayerNorm consumer fold on the QKV GEMM."""
+    rng = np.random.default_rng(31 + S)
+    m = zoo.bert(layers=2)
+    ids, mask = bert_inputs(rng, 3, S, pad_from=pad_from)
+    ref = cpu_inference(m, [ids, mask])[0]
+    monkeypatch.setenv("SPI_LN_FOLD", fold)
+    fused = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", max_batch=3, seq_len=128), [ids, mask], ref.shape)
+    monkeypatch.setenv("SPI_QKV_ATTN", "0")
+    plain = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", max_batch=3, seq_len=128), [ids, mask], ref.shape)
+    d = normalized_max_error(fused, plain)
+    e = normalized_max_error(fused, ref)
+    print(f"qkv+attention fused S{S} pad{pad_from} fold{fold}: vs unfused {d:.3e} (identical: {np.array_equal(fused, plain)}), "
+          f"vs oracle {e:.3e}")
+    assert e < 1e-3 and d < 2e-4, (e, d)
+
+
 def test_affine_codelet_like_reference(spi, gpu):
     """x + 1.5 on {1,2,3} (tests/unit/core/unit_starpu_setup.cpp:2332-2433)."""
     rep = spi.ModelReplica(None, 0, "fp32", max_batch=3, family="affine", affine=(1.0, 1.5))
