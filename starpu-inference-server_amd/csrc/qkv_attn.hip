@@ -6,8 +6,8 @@
 //      pre-LayerNorm rows when the LayerNorm is folded -- ln_fold.hpp's consumer epilogue)
 //      times the head's 192 packed QKV weight rows (q | k | v, 64 each), K = D.  Both operands
 //      go HBM -> LDS by LDS-DMA (1 KiB pieces, 5 per wave per 64-deep k-step, the XOR swizzle on
-//      the source address) through a 3-stage ring (120 KiB); waves 2 (rows) x 4 (columns), a
-//      64 x 48 output block each, v_mfma_f32_16x16x32_f16.
+//      the source address) through a 2-stage ring (80 KiB: two workgroups per CU); waves 2 (rows)
+//      x 4 (columns), a 64 x 48 output block each, v_mfma_f32_16x16x32_f16.
 //   2. Epilogue: bias (+ the fold's rstd (acc - mean c1)) and the fp16 rounding the unfused
 //      QKV GEMM applies, into LDS as Q / K / V [128][72] (144-byte rows) over the ring.
 //   3. Attention on the LDS-resident Q / K / V: attention.hip's swapped orientation (S^T = K Q^T,
@@ -35,16 +35,14 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr int HD = 64;                      // head dim
 constexpr int QR = 128;                     // token rows per workgroup (S <= 128)
 constexpr int QC = 3 * HD;                  // q | k | v columns of one head
-constexpr int STG = 3;                      // ring stages
 constexpr int A_BYTES = QR * 128;           // one 64-deep k-step of A: 16 KiB
 constexpr int STAGE = A_BYTES + QC * 128;   // + W: 40 KiB
 constexpr int PIECES = (QR + QC) / 8;       // 1 KiB LDS-DMA pieces per stage (40)
 constexpr int PPW = PIECES / 8;             // per wave (5)
 constexpr int LDQ = HD + 8;                 // Q / K / V row stride in elements (144 B)
 constexpr int QKV_BYTES = 3 * QR * LDQ * 2; // 54 KiB, over the ring after the k-loop
-constexpr int STATS_OFF = STG * STAGE;      // the rows' {mean, rstd} (fold) past the ring
-constexpr int LDS_BYTES = STATS_OFF + QR * 8;
-static_assert(PIECES % 8 == 0 && QKV_BYTES <= STATS_OFF, "tile geometry");
+constexpr int STATS_OFF = QKV_BYTES;        // the rows' {mean, rstd} (fold), after the k-loop too
+static_assert(PIECES % 8 == 0 && STATS_OFF + QR * 8 <= 2 * STAGE, "tile geometry");
 
 struct QkvAttnArgs {
   const _Float16* A;  // [B S][lda] fp16 rows
@@ -66,9 +64,11 @@ __device__ __forceinline__ void wait_vm_bar() {
   asm volatile("" ::: "memory");
 }
 
-template <bool LNC>
+// STG ring stages: 3 (120 KiB, stage t + 2 in flight while t computes) or 2 (80 KiB: two
+// workgroups fit a CU)
+template <bool LNC, int STG>
 __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[STG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x / g.H, h = blockIdx.x - b * g.H;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
     for (int c = 0; c < 16; ++c) ch[c] = c < g.ln_chunks ? ch[c] : float2{0.f, 0.f};
   }
   stage(0);
-  stage(1);  // KT >= 2 (checked on the host): no branch, so the loads' wait stays counted
+  if constexpr (STG == 3) stage(1);  // KT >= 2 (checked on the host): no branch, so the loads' wait stays counted
   [[maybe_unused]] float2 row_st = float2{0.f, 0.f};  // thread tid < 128: row tid's {mean, rstd}
   if constexpr (LNC) {
     {  // ln_row_stats' arithmetic (Chan) on the loaded partials; chunks <= 16 (D <= 1024); branch-free
@@ -146,13 +146,14 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
     return *reinterpret_cast<const half8*>(img + row * 128 + ((c ^ (row & 7)) << 4));
   };
   for (int t = 0; t < KT; ++t) {
-    // stage t landed (stage t + 1's pieces may stay in flight); every wave is past step t - 1's
-    // reads, so the buffer of t + 2 (= that of t - 1) is free
-    if (t + 1 < KT)
+    // STG = 3: stage t landed (stage t + 1's pieces may stay in flight); every wave is past step
+    // t - 1's reads, so the buffer of t + 2 (= that of t - 1) is free.  STG = 2: stage t landed,
+    // then stage t + 1 goes into the buffer of t - 1.
+    if (STG == 3 && t + 1 < KT)
       wait_vm_bar<PPW>();
     else
       wait_vm_bar<0>();
-    if (t + 2 < KT) stage(t + 2);
+    if (t + STG - 1 < KT) stage(t + STG - 1);
     const char* buf = lds + (t % STG) * STAGE;
     half8 fa[2][4], fb[2][3];
 #pragma unroll
@@ -322,10 +323,12 @@ void qkv_attention(const void* A, int lda, const void* W, int ldw, const float* 
   g.ln_eps = ln_eps;
   g.scale = scale;
   const dim3 grid(B * heads), blk(512);
+  // two stages (80 KiB: two workgroups per CU): BERT-base bs8 four streams 24.7-24.8k seq/s
+  // against 24.0k with three (120 KiB) and 23.3-23.4k unfused (profiles/r05/qkv_attn/)
   if (ln_stats)
-    SPI_LAUNCH(qkv_attn_kernel<true>, grid, blk, 0, s, g);
+    SPI_LAUNCH((qkv_attn_kernel<true, 2>), grid, blk, 0, s, g);
   else
-    SPI_LAUNCH(qkv_attn_kernel<false>, grid, blk, 0, s, g);
+    SPI_LAUNCH((qkv_attn_kernel<false, 2>), grid, blk, 0, s, g);
 }
 
 }  // namespace spi
