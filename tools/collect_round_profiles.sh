@@ -10,9 +10,9 @@ r=${1:?round, e.g. r04}
 dst=profiles/$r
 mkdir -p "$dst"
 cp gpurun_out/trace/trace_*_ops.csv gpurun_out/trace/trace_*_kernel_stats.csv "$dst/" 2>/dev/null || true
-if [ -f gpurun_out/rl4/roofline_rocprof.json ]; then
-  cp gpurun_out/rl4/roofline_rocprof.json "$dst/roofline_rocprof.json"
-  cp gpurun_out/rl4/roofline_*_kernel_stats.csv "$dst/" 2>/dev/null || true
+if [ -f gpurun_out/rl_$r/roofline_rocprof.json ]; then
+  cp gpurun_out/rl_$r/roofline_rocprof.json "$dst/roofline_rocprof.json"
+  cp gpurun_out/rl_$r/roofline_*_kernel_stats.csv "$dst/" 2>/dev/null || true
 fi
 for d in gpurun_out/pmc_*; do
   [ -d "$d" ] || continue

@@ -1,30 +1,31 @@
 #!/usr/bin/env bash
-# Round-4 roofline evidence for every BASELINE GPU config (run through gpurun from the repo root):
+# Roofline evidence of a round (ROUND=r05 by default) for every BASELINE GPU config (run through gpurun from the repo root):
 #   1. tools/trace_round.sh: rocprofv3 kernel trace of each config's graph-replayed timed loop,
 #      regrouped per op (gpurun_out/trace/trace_<cfg>_ops.csv + kernel stats);
-#   2. the trace CSVs copied into profiles/r04/ of this (scratch) tree, so bench.py's roofline
+#   2. the trace CSVs copied into profiles/$ROUND/ of this (scratch) tree, so bench.py's roofline
 #      picks each config's op from them (bench.trace_ranking) -- copy them into the repo too;
 #   3. per config, rocprofv3 --kernel-trace --stats of `bench.py --roofline-only` for the top op
-#      of its trace (the back-to-back launches the bench line times) -> gpurun_out/rl4/
+#      of its trace (the back-to-back launches the bench line times) -> gpurun_out/rl_$ROUND/
 #      roofline_rocprof.json (tools/rocprof_roofline.py) + roofline_<cfg>_kernel_stats.csv.
 # usage: bash tools/round4_profile.sh
 set -euo pipefail
+ROUND=${ROUND:-r05}
 export TMPDIR=/tmp
 cfgs=(resnet18:8:fp16m bert_base:8:fp16 resnet152:32:fp16x3 vit_l_16:16:fp16)
-if [ "${SKIP_TRACE:-0}" != 1 ]; then  # SKIP_TRACE=1: the committed profiles/r04 traces pick the ops
+if [ "${SKIP_TRACE:-0}" != 1 ]; then  # SKIP_TRACE=1: the committed profiles/$ROUND traces pick the ops
   mkdir -p gpurun_out/trace
   bash tools/trace_round.sh "${cfgs[@]}" > gpurun_out/trace/log.txt 2>&1
-  mkdir -p profiles/r04
-  cp gpurun_out/trace/trace_*_ops.csv profiles/r04/
+  mkdir -p profiles/$ROUND
+  cp gpurun_out/trace/trace_*_ops.csv profiles/$ROUND/
 fi
-out=gpurun_out/rl4
+out=gpurun_out/rl_$ROUND
 mkdir -p "$out"
 for c in "${cfgs[@]}"; do
   IFS=: read -r model batch prec <<< "$c"
   tag="${model}_bs${batch}_${prec}"
-  op=$(python3 - "$tag" <<'EOF'
+  op=$(python3 - "$tag" "$ROUND" <<'EOF'
 import csv, sys
-rows = [r for r in csv.DictReader(open(f"profiles/r04/trace_{sys.argv[1]}_ops.csv")) if r["op"]]
+rows = [r for r in csv.DictReader(open(f"profiles/{sys.argv[2]}/trace_{sys.argv[1]}_ops.csv")) if r["op"]]
 rows.sort(key=lambda r: -float(r["total_us"]))
 print(rows[0]["op"].split("|")[0])
 EOF
