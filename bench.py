@@ -442,16 +442,18 @@ def cpu_baseline(model, name, batch, seconds):
 
 
 def config_line(spi, zoo, rtmod, name, batch, precision, workers, streams, steps, dev, rank, world, dist, seq=128,
-                e2e_requests=400):
+                e2e_requests=400, tasks_per_step=1):
     """Device-resident inf/s (all ranks), loaded p50 task latency and roofline (rank 0), and the
-    PCIe-inclusive e2e run (all ranks, aggregated) for one BASELINE config."""
+    PCIe-inclusive e2e run (all ranks, aggregated) for one BASELINE config.  A step is
+    `tasks_per_step` codelet calls per worker stream, as the headline's."""
     model = zoo.build(name, seed=0)
     rep = spi.ModelReplica(model, dev, precision, max_batch=batch, seq_len=seq if name.startswith("bert") else 0,
                            graphs=True)
     h = Harness(spi, rep, name, dev, batch, workers, np.random.default_rng(3 + rank), streams)
-    el = h.throughput(steps, 2, 1, world, dist)
+    el = h.throughput(steps, 2, tasks_per_step, world, dist)
     lat = h.loaded_latency(10)
-    out = {"value": round(world * workers * batch * steps / el, 2),
+    out = {"value": round(world * workers * tasks_per_step * batch * steps / el, 2), "steps": steps,
+           "tasks_per_step": tasks_per_step,
            "unit": "sequences/s" if name.startswith("bert") else "inferences/s", "dtype": precision, "batch": batch,
            "n_gpus": world, "p50_task_latency_ms": round(percentile(lat, 50), 4),
            "gflop_per_inference": round(rep.flops(1) / 1e9, 3)}
@@ -708,7 +710,8 @@ def main():
                 dist.barrier()
             extras[key] = config_line(spi, zoo, rtmod, name, b, prec, args.workers, h.streams,
                                       max(10, args.steps // 2), dev, rank, world, dist,
-                                      e2e_requests=400 if name != "bert_base" else 1000)
+                                      e2e_requests=400 if name != "bert_base" else 1000,
+                                      tasks_per_step=args.tasks_per_step)
         result["extras"] = extras
 
     if world > 1:
