@@ -1621,7 +1621,6 @@ int estep_of(Prec prec) {
 // 128x128 rings, 4-stage halo rings, XCD-local split-K, per-knob ring depths,
 // DESIGN.md 6) are gone; what remains:
 //   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM (sweeps)
-//   SPI_GEMM_POLICY=tput:T               plan target T workgroups (default 128)
 //   SPI_GEMM_MAXSPLIT=S                  cap split-K (1: none)
 //   SPI_GEMM_HALO_CFG                    halo candidates: "0" off, "rows,a|s" forced,
 //                                        "OW:rows,a|s;..." per map width
@@ -1637,7 +1636,6 @@ struct Knobs {
   // ... else with >= T128 tiles of 128 x 256 -> gemm256's 128-row tile (round 5; 0 = off)
   int g128_min = 0;  // off by default: under the four worker streams BERT -7 %, ViT-L -1 %
   int g128_nbuf = 3;  // third field: k-tile buffers of the 128-row tile (2: 96 KiB, 3: 144 KiB)
-  int g128_kmin = 0, g128_kmax = 1 << 30;  // fourth / fifth: K range of the 128-row route
   // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
   // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
   // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
@@ -1675,13 +1673,9 @@ Knobs read_knobs() {
       }
     }
   }
-  if (const char* e = std::getenv("SPI_GEMM_POLICY"); e && std::strncmp(e, "tput:", 5) == 0)
-    k.target = std::max(1, std::atoi(e + 5));
   if (const char* e = std::getenv("SPI_GEMM_256_MIN"); e && *e) {
-    int a = 0, b = 0, c = 3, kmin = 0, kmax = 1 << 30;
-    const int n = std::sscanf(e, "%d,%d,%d,%d,%d", &a, &b, &c, &kmin, &kmax);
-    k.g128_kmin = kmin;
-    k.g128_kmax = kmax;
+    int a = 0, b = 0, c = 3;
+    const int n = std::sscanf(e, "%d,%d,%d", &a, &b, &c);
     k.g256_min = a;
     if (n >= 2) k.g128_min = b;
     if (n >= 3) k.g128_nbuf = c == 2 ? 2 : 3;
@@ -1737,7 +1731,7 @@ int route_bm(const GemmDesc& d, Prec prec) {
   const Knobs& k = knobs();
   if (prec != Prec::F16) return 0;
   if (gemm256_eligible(d, prec, k.g256_min)) return 256;
-  if (d.K >= k.g128_kmin && d.K <= k.g128_kmax && gemm256_eligible(d, prec, k.g128_min, 128)) return 128;
+  if (gemm256_eligible(d, prec, k.g128_min, 128)) return 128;
   if (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k && gemm256_eligible(d, prec, k.g256_longk_tiles)) return 256;
   return 0;
 }

@@ -374,9 +374,6 @@ struct spi_runtime {
   std::vector<std::unique_ptr<SlotPool>> pools;
   std::vector<std::unique_ptr<Worker>> workers;
   std::unique_ptr<CopyPool> copier;
-  // SPI_RT_COMPLETION=spin: finalize polls the completion event (yielding) instead of
-  // hipEventSynchronize (read at create)
-  bool spin_completion = false;
   std::mutex mu;
   std::condition_variable cv_job, cv_idle;
   std::map<QueueKey, Job> queue;
@@ -611,12 +608,7 @@ void spi_runtime::finalize_oldest(Worker* w) {
   SlotPool& pool = *pools[w->pool];
   Slot& slot = pool.slots[t.slot];
   const int64_t e0 = now_ns();
-  hipError_t se;
-  if (spin_completion) {
-    while ((se = hipEventQuery(slot.done)) == hipErrorNotReady) std::this_thread::yield();
-  } else {
-    se = hipEventSynchronize(slot.done);
-  }
+  const hipError_t se = hipEventSynchronize(slot.done);
   if (se != hipSuccess && t.status == SPI_OK) {
     t.status = SPI_ERR_DEVICE;
     t.err = "stream synchronisation failed";
@@ -975,7 +967,6 @@ spi_runtime* spi_runtime_create(const spi_runtime_config* c, char* err, size_t e
   }
   rt->warmup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - warm_t0).count();
   rt->copier = std::make_unique<CopyPool>(cfg.copy_threads - 1);
-  if (const char* e = std::getenv("SPI_RT_COMPLETION"); e && std::strcmp(e, "spin") == 0) rt->spin_completion = true;
   rt->last_target = cfg.max_batch;
   for (auto& w : rt->workers) w->thread = std::thread(&spi_runtime::run, rt.get(), w.get());
   return rt.release();

@@ -3,7 +3,7 @@
 process, rounds interleaved (the bench's timed loop: `--workers` worker streams
 replaying the captured forward back to back).
 
-Each policy is a set of environment knobs read by the library (SPI_GEMM_POLICY,
+Each policy is a set of environment knobs read by the library (SPI_GEMM_256_MIN,
 SPI_GEMM_HALO_CFG, SPI_GEMM_MAXSPLIT, ...); the knobs are re-read and a fresh
 replica (fresh graphs) is built per policy.
 
@@ -20,8 +20,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KNOBS = ["SPI_STEM_FUSED", "SPI_GEMM_256_MIN", "SPI_GEMM_256_LONGK", "SPI_GEMM_POLICY", "SPI_GEMM_HALO_CFG", "SPI_GEMM_WIN",
-         "SPI_GEMM_MAXSPLIT", "SPI_GEMM_PLAN", "SPI_CONV_WRES", "SPI_LN_FOLD"]
+KNOBS = ["SPI_STEM_FUSED", "SPI_GEMM_256_MIN", "SPI_GEMM_256_LONGK", "SPI_GEMM_HALO_CFG", "SPI_GEMM_WIN",
+         "SPI_GEMM_MAXSPLIT", "SPI_GEMM_PLAN", "SPI_CONV_WRES", "SPI_LN_FOLD", "SPI_QKV_ATTN"]
 
 
 def parse(p):
