@@ -154,6 +154,15 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
+// Diagnostic build -DSPI_G256_TIMELINE (tools/g256_timeline.py): per workgroup, s_memrealtime at
+// entry, after the prologue's first wait, after the k-loop and at exit, plus HW_ID / XCC_ID.
+#ifdef SPI_G256_TIMELINE
+__device__ unsigned long long g_g256_tl[8192 * 6];
+#define G256_RT(x) x = __builtin_amdgcn_s_memrealtime()
+#else
+#define G256_RT(x)
+#endif
+
 // Ping-pong wave rows (the lock-step two-tile-ahead variant measured C5 -2.3 % and was removed, round 4)
 template <int RES, int BM, int NBUF>
 __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
@@ -169,6 +178,24 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   int* const s_ticket = reinterpret_cast<int*>(lds);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  [[maybe_unused]] unsigned long long tl0 = 0, tl1 = 0, tl2 = 0;
+  G256_RT(tl0);
+  // every return of the kernel goes through exit_stamp()
+  auto exit_stamp = [&]() {
+#ifdef SPI_G256_TIMELINE
+    unsigned long long tl3;
+    G256_RT(tl3);
+    if (tid == 0 && blockIdx.x < 8192) {
+      unsigned long long* o = g_g256_tl + (size_t)blockIdx.x * 6;
+      o[0] = tl0;
+      o[1] = tl1;
+      o[2] = tl2;
+      o[3] = tl3;
+      o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+#endif
+  };
   const int fr = lane & 15, fq = lane >> 4;
 
   // XCD-aware bijective remap: the workgroups one XCD receives get consecutive ids (slice-major:
@@ -276,6 +303,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     else
       vm_wait_nolgkm<4>();
     if (wr == 1) bar();  // the skew
+    G256_RT(tl1);
     auto ktile = [&](int kt, auto rem_c) {
       constexpr int R = decltype(rem_c)::value;
       const char* buf = bufof(kt);
@@ -334,6 +362,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     else
       vm_wait_nolgkm<2>();
     if (wr == 1) bar();  // the skew
+    G256_RT(tl1);
     auto ktile = [&](int kt, auto rem_c) {
       constexpr int R = decltype(rem_c)::value;
       const char* buf = bufof(kt);
@@ -378,6 +407,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     else
       vm_wait_nolgkm<2>();
     if (wr == 1) bar();  // the skew
+    G256_RT(tl1);
     auto ktile = [&](int kt, auto rem_c) {
       constexpr int R = decltype(rem_c)::value;
       const char* buf = bufof(kt);
@@ -405,6 +435,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (wr == 0) bar();  // the skew, closed
   }
 
+  G256_RT(tl2);
   if (g.splits > 1) {
     // Split-K hand-off, gemm.hip's protocol (tickets first; slices that are not last publish
     // their partial write-through (sc1) in fragment order -- thread tid's accumulator (a, b) is
@@ -429,6 +460,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
                                                  (slice * SLAB + ((a * 4 + b) * 512 + tid) * 4) * 4, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
       if (tid == 0) __hip_atomic_fetch_add(words + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      exit_stamp();
       return;
     }
     if (tid == 0) {
@@ -498,6 +530,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
             static_cast<_Float16*>(g.C)[ci] = static_cast<_Float16>(y);
         }
       }
+    exit_stamp();
     return;
   }
   // The walk is branch-free per row: the residual kind (none / fp16 / fp32) is a template
@@ -560,8 +593,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     }
 #pragma unroll
     for (int h = 0; h < kRounds; ++h) {
-      // residual rows: the first half of the round's prefetched, the rest loaded inside the
-      // walk (all eight would spill next to the accumulators the other wave row still holds)
+      // residual rows: a ring of four rows per thread, the first four loaded before the park
+      // (all eight at once would spill next to the accumulators the other wave row still holds)
       constexpr int PRE = 4;
       half8 rvh[RES == 1 ? PRE : 1];
       floatx4 rvf[RES == 2 ? PRE : 1][2];
@@ -605,23 +638,25 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           const float* src = T + row * 256 + ((8 * cg) ^ (((row >> 2) & 3) << 4));
           const floatx4 x0 = *reinterpret_cast<const floatx4*>(src);
           const floatx4 x1 = *reinterpret_cast<const floatx4*>(src + 4);
+          // residual rows through a ring of PRE slots: slot pass % PRE is consumed here and
+          // refilled with row pass + PRE, so every load has PRE passes to land (round 5: the
+          // passes past PRE had loaded their rows in the walk, latency exposed -- ViT-L
+          // out-proj / FFN2 epilogues 10.3-10.5 us, tools/g256_timeline.py)
           float r[8] = {};
           if constexpr (RES == 1) {
-            const half8 q = pass < PRE ? rvh[pass % PRE]
-                                       : *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) +
-                                                                         res_row(pass));
+            const half8 q = rvh[pass % PRE];
+            if (pass + PRE < kPasses)
+              rvh[pass % PRE] = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) +
+                                                               res_row(pass + PRE));
 #pragma unroll
             for (int e = 0; e < 8; ++e) r[e] = static_cast<float>(q[e]);
           }
           if constexpr (RES == 2) {
-            floatx4 q0, q1;
-            if (pass < PRE) {
-              q0 = rvf[pass % PRE][0];
-              q1 = rvf[pass % PRE][1];
-            } else {
-              const float* rp = static_cast<const float*>(g.res) + res_row(pass);
-              q0 = *reinterpret_cast<const floatx4*>(rp);
-              q1 = *reinterpret_cast<const floatx4*>(rp + 4);
+            const floatx4 q0 = rvf[pass % PRE][0], q1 = rvf[pass % PRE][1];
+            if (pass + PRE < kPasses) {
+              const float* rp = static_cast<const float*>(g.res) + res_row(pass + PRE);
+              rvf[pass % PRE][0] = *reinterpret_cast<const floatx4*>(rp);
+              rvf[pass % PRE][1] = *reinterpret_cast<const floatx4*>(rp + 4);
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -706,12 +741,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   if constexpr (RES == 0) {
     if (g.ln_in_chunks > 0) {
       by_act(F{}, T1{}, F{});
+      exit_stamp();
       return;
     }
   }
   if constexpr (RES == 2) {
     if (g.ln_out) {
       by_act(T1{}, F{}, T1{});
+      exit_stamp();
       return;
     }
   }
@@ -719,11 +756,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     by_act(T1{}, F{}, F{});
   else
     by_act(F{}, F{}, F{});
+  exit_stamp();
 }
 
 }  // namespace
 
 void gemm256_reload_env() {}
+
+#ifdef SPI_G256_TIMELINE
+extern "C" int spi_debug_g256_timeline(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_g256_tl), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int gemm256_splits(const GemmDesc& d, int target, int max_split, int bm) {
   const int tiles = (d.M + bm - 1) / bm * (d.N / 256), kt = d.K / 64;
