@@ -350,34 +350,44 @@ constexpr int kWinRows = BM + 8;
 // row statistics, computed once per row before the epilogue's walk).
 template <int BM, int KIND>
 constexpr int kLnBytes = KIND == kDense ? 2 * BM * 8 : 0;
+// Window kind with NW = 8 (round 5): two K groups of 4 waves in one workgroup, each walking
+// half of the slice's super-steps through its own LDS (ring + windows) and reducing through
+// LDS at the end -- the intra-workgroup split-K of DESIGN.md 3.1.6.
+template <int KIND, int NW>
+constexpr int kKGroups = KIND == kConvTapW && NW == 8 ? 2 : 1;
+// LDS bytes of one K group (the whole workgroup: kKGroups times this)
 template <int BM, int BN, int STAGES, int KIND, int NW>
 constexpr int kLdsBytes = kIsHalo<KIND> ? STAGES * BN * 128 + 2 * kHaloHQ<BM, KIND, NW> * NW * 8 * 128 + 16
                           : KIND == kConvTapW ? STAGES * BN * 128 + 2 * kWinRows<BM> * 128 + 16
                                               : STAGES * (BM + BN) * 128 + kLnBytes<BM, KIND> + 16;
 // Occupancy asked of the register allocator: 4 / 3 / 2 waves per SIMD by tile
-// size per wave, capped by what the tile's LDS ring allows (NW / 4 waves per SIMD
-// per block, 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
+// size per wave (of a K group), capped by what the tile's LDS ring allows (NW / 4 waves
+// per SIMD per block, 160 KiB of LDS per CU; RB = 128 bytes per row per stage in every mode).
 template <int BM, int BN, int STAGES, int KIND, int NW>
 constexpr int kMinWaves = std::max(
-    1, std::min(BM * BN * 4 / NW <= 64 * 64 ? 4 : BM * BN * 4 / NW <= 128 * 64 ? 3 : 2,
-                (160 * 1024) / kLdsBytes<BM, BN, STAGES, KIND, NW> * NW / 4));
+    1, std::min(BM * BN * 4 * kKGroups<KIND, NW> / NW <= 64 * 64 ? 4 : BM * BN * 4 * kKGroups<KIND, NW> / NW <= 128 * 64 ? 3 : 2,
+                (160 * 1024) / (kKGroups<KIND, NW> * kLdsBytes<BM, BN, STAGES, KIND, NW>) * NW / 4));
 
 // NW waves per workgroup in an (NW / 2) x 2 grid over the tile: wave (wm, wn)
 // owns rows [wm * BM / (NW / 2), ...) x columns [wn * BN / 2, ...).
 // The workgroup body: problem `a`, split-K slice `kslice`, linear tile `lin`.
 // gemm_kernel passes its own arguments (constant kernarg offsets, preloadable);
 // gemm_kernel_pair selects one of two problems at run time.
-template <int MODE, int BM, int BN, int STAGES, int KIND, int NW>
+template <int MODE, int BM, int BN, int STAGES, int KIND, int NWA>
 __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, const int lin, const int hl) {
   constexpr bool CONV = KIND != kDense;
   constexpr bool TAP = KIND == kConvTap;
   constexpr bool HALO = kIsHalo<KIND>;
   constexpr bool WIN = KIND == kConvTapW;
   constexpr bool AR = !HALO && !WIN;  // A tiles go through the ring
-  static_assert(!WIN || ((BM == 64 || BM == 128) && BN == 64 && NW == 4 && STAGES == 3),
-                "window kind: 64 / 128 x 64 tiles, 4 waves, 3 W stages");
-  constexpr int NT = 64 * NW;  // threads per workgroup
-  static_assert(NW == 4 || NW == 8, "4- or 8-wave workgroups");
+  static_assert(!WIN || ((BM == 64 || BM == 128) && BN == 64 && STAGES == 3),
+                "window kind: 64 / 128 x 64 tiles, 3 W stages");
+  static_assert(NWA == 4 || NWA == 8, "4- or 8-wave workgroups");
+  // KG K groups of NW waves: everything below is one group's (its waves, threads, LDS)
+  constexpr int KG = kKGroups<KIND, NWA>;
+  constexpr int NW = NWA / KG;
+  static_assert(NW == 4 || NW == 8, "waves per K group");
+  constexpr int NT = 64 * NW;  // threads per K group
   using TR = Traits<MODE>;
   using AT = typename TR::A;
   constexpr int ESTEP = TR::ESTEP, EPC = TR::EPC, RB = TR::RB;
@@ -395,7 +405,10 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   static_assert(LDSB == STAGES * IMG + 2 * HBUF + kLnBytes<BM, KIND> + 16, "LDS layout");
   static_assert(!WIN || RB == 128, "window rows are 128-byte pixel blocks");
   static_assert(!HALO || (STAGES >= 3 && STAGES <= 6 && RPI == 8), "halo: 9 taps, the next halo at tap 10 - STAGES");
-  __shared__ __attribute__((aligned(16))) char lds[LDSB];
+  __shared__ __attribute__((aligned(16))) char lds_wg[KG * LDSB];
+  // K group (an SGPR) and its LDS: [0, LDSB) for group 0, [LDSB, 2 LDSB) for group 1
+  const int grp = KG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT);
+  char* const lds = KG == 1 ? lds_wg : lds_wg + grp * LDSB;
   int* s_flag = reinterpret_cast<int*>(lds + LDSB - 16);
   [[maybe_unused]] unsigned long long rt_e = 0, rt_l0 = 0, rt_l1 = 0, rt_p1 = 0, rt_p2 = 0;
   SPI_RT(rt_e);
@@ -423,7 +436,8 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
 
   const GemmDesc& d = a.d;
   // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar math.
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = KG == 1 ? (int)threadIdx.x : (int)threadIdx.x & (NT - 1), lane = tid & 63,
+            wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware remap: consecutive tiles (same weight columns) land on one XCD's L2.
   // hl: the workgroup's dispatch index inside this problem's range; the hardware deals
   // dispatch indices round-robin to the 8 XCDs, so hl & 7 names the XCD.  Number each
@@ -499,8 +513,17 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     return (ty < a.h_th && img < a.imgs && (unsigned)oy < (unsigned)d.OH) ? (img * d.OH + oy) * d.OW + tx
                                                                                       : -1;
   };
-  const int kbeg = kslice * a.k_per_split;
-  const int kend = min(d.Kpad, kbeg + a.k_per_split);
+  int kbeg = kslice * a.k_per_split;
+  int kend = min(d.Kpad, kbeg + a.k_per_split);
+  if constexpr (KG == 2) {
+    // K groups: the first / second half of the slice's super-steps (the host plans an even
+    // count per slice, so both groups run the same number of steps -- and of barriers)
+    const int half = (kend - kbeg) / (6 * ESTEP) * (3 * ESTEP);
+    if (grp == 0)
+      kend = kbeg + half;
+    else
+      kbeg += half;
+  }
   // halo: channel blocks [h_b0, h_b1) of this split-K slice, 9 taps each
   const int h_b0 = HALO ? kslice * a.h_bps : 0;
   const int h_b1 = HALO ? min(a.h_nblk, h_b0 + a.h_bps) : 0;
@@ -804,7 +827,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   [[maybe_unused]] const bool rpf_tile = RPF && a.p.res && a.vec_ok && n0 + BN <= d.N && !d.pool_rows;
   // (window kind: into the window buffer the last super-step does not use -- 9 KiB, so fp16
   // residual rows only -- and the tile parks at 0)
-  [[maybe_unused]] const bool rpf_loop = rpf_tile && a.splits == 1 && (!WIN || res_rb == 128);
+  [[maybe_unused]] const bool rpf_loop = rpf_tile && a.splits == 1 && (!WIN || res_rb == 128) && grp == 0;
   [[maybe_unused]] const int rpf_step = max(0, nsteps - STAGES + 1);
   [[maybe_unused]] const int rpf_off = WIN ? STAGES * IMG + ((nsteps / 3) & 1) * HBUF : (nsteps % STAGES) * IMG;
   [[maybe_unused]] const int park_off = WIN ? 0 : ((nsteps - 1) % STAGES) * IMG;
@@ -1493,7 +1516,7 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   SPI_STAMP(st_d);
   SPI_RT(rt_l1);
 #ifdef SPI_GEMM_STAMPS
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     unsigned long long* gs = g_gemm_stamps + (size_t)(blockIdx.x & 65535) * 8;
     gs[0] = st_d - st_t0;
     gs[1] = st_wait;
@@ -1502,6 +1525,26 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     gs[4] = (unsigned long long)nsteps;
   }
 #endif
+  if constexpr (KG == 2) {
+    // K groups: group 1 parks its partial in fragment order (thread t's accumulator (i, j) is
+    // 16 contiguous bytes at ((i TJ + j) NT + t) 16) in its own W stages 0-1 -- free since the
+    // last step's barrier (that step reads stage 2 and a window) -- and exits; group 0 adds it
+    // to its own and goes on alone (s_barrier waits for the surviving waves only).
+    static_assert(TI * TJ * NT * 16 <= 2 * IMG, "group 1's partial fits its W stages 0-1");
+    floatx4* const part = reinterpret_cast<floatx4*>(lds_wg + LDSB);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) part[(i * TJ + j) * NT + tid] = acc[i][j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (grp == 1) return;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] += part[(i * TJ + j) * NT + tid];
+  }
   if (!kSplitK<BM, BN, KIND> || a.splits == 1) {
     if (RPF && rpf_loop)
       finish(acc, park_off, lds + rpf_off);
@@ -1631,7 +1674,9 @@ struct Knobs {
   int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
   int max_split = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
-  int win = 1;   // SPI_GEMM_WIN=0: 3x3/s1 tap walks without the kw window (kConvTapW)
+  // SPI_GEMM_WIN=0: 3x3/s1 tap walks without the kw window (kConvTapW); 2 / 3: 64 x 64 window
+  // tiles as two K groups of 4 waves (8-wave workgroups), at the 4-wave plan's slices / half of them
+  int win = 1;
   int g256_min = 128;      // SPI_GEMM_256_MIN="T256[,T128]": dense F16 GEMMs with >= T256 tiles of 256^2 -> gemm256 (0 = off)
   // ... else with >= T128 tiles of 128 x 256 -> gemm256's 128-row tile (round 5; 0 = off)
   int g128_min = 0;  // off by default: under the four worker streams BERT -7 %, ViT-L -1 %
@@ -1714,7 +1759,7 @@ Knobs read_knobs() {
     }
   }
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("SPI_GEMM_WIN"); e && *e) k.win = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SPI_GEMM_WIN"); e && *e) k.win = std::max(0, std::min(3, std::atoi(e)));
   return k;
 }
 
@@ -1898,6 +1943,15 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   const Plan pl = finish_plan(Plan{64, 64, stages_for((ksteps + sp - 1) / sp), sp, 0}, ksteps, ES, d.krep);
   if (window_ok(d, prec)) {
     // the kw-window tap walk: slices of whole (kh, channel block) super-steps
+    if (k.win >= 2 && ksteps % 6 == 0) {
+      // two K groups per workgroup (8 waves): slices of an even number of super-steps,
+      // SPI_GEMM_WIN=2 at the 4-wave plan's slice count, 3 at half of it
+      const int sp2 = k.win == 3 ? (sp + 1) / 2 : sp;
+      Plan w = finish_plan(Plan{64, 64, 3, sp2, 0}, ksteps, ES, 6);
+      w.win = 1;
+      w.nw = 8;
+      return w;
+    }
     Plan w = finish_plan(Plan{64, 64, 3, sp, 0}, ksteps, ES, 3);
     w.win = 1;
     return w;
@@ -1995,7 +2049,13 @@ void dispatch(const Plan& pl, const KArgs& g, hipStream_t s) {
   }
   if (pl.win) {
     if constexpr (MODE == (int)Prec::F16 || MODE == kF16X3S) {
-      if (pl.bm == 128)
+      if (pl.nw == 8) {
+        // K groups: both must walk the same number of super-steps (their barriers pair up)
+        const int ES = Traits<MODE>::ESTEP;
+        if (pl.bm != 64 || pl.k_per_split % (6 * ES) || g.d.Kpad % (6 * ES))
+          throw std::logic_error("window kind with K groups: slices of an even number of super-steps");
+        SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvTapW, 8>), grid, dim3(512), 0, s, g);
+      } else if (pl.bm == 128)
         SPI_LAUNCH((gemm_kernel<MODE, 128, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);
       else
         SPI_LAUNCH((gemm_kernel<MODE, 64, 64, 3, kConvTapW>), grid, dim3(256), 0, s, g);

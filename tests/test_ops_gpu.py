@@ -179,8 +179,9 @@ def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
     BM + 2 consecutive pixels, taps in the padding zeroed at fragment read -- every 64x64 and
     128x64 tap plan of such a conv (split-K slices of whole (kh, channel block) super-steps; ragged M, maps 3 to
     28 wide, several images per tile).  Checked against an fp32 conv and against the plain tap
-    walk (SPI_GEMM_WIN=0); halo kinds and the weight-resident 64->64 conv off so every shape
-    takes it."""
+    walk (SPI_GEMM_WIN=0) and with the 64-row tiles as two K groups of 4 waves (SPI_GEMM_WIN=2 /
+    3, round 5: 8-wave workgroups reducing through LDS); halo kinds and the weight-resident
+    64->64 conv off so every shape takes it."""
     import os
     g = torch.Generator().manual_seed(B * 7 + H * 3 + cin + cout)
     x = torch.randn(B, H, H, cin, generator=g)
@@ -205,14 +206,21 @@ def test_conv3x3_window_kind(ops, prec, B, H, cin, cout, res):
     try:
         os.environ["SPI_GEMM_HALO_CFG"] = "0"
         os.environ["SPI_CONV_WRES"] = "0"
-        for win in ("1", "0"):
+        for win in ("1", "0", "2", "3"):
             os.environ["SPI_GEMM_WIN"] = win
             ops.lib.spi_debug_gemm_reload_env()
             pl = conv_plan(ops, 3 if split else 1, B, H, cin, cout)
-            assert pl["win"] == int(win) and pl["bm"] in (64, 128), pl
-            if win == "1":
+            assert pl["win"] == min(1, int(win)) and pl["bm"] in (64, 128), pl
+            if win != "0":
                 tiles128 = -(-B * H * H // 128) * -(-cout // 64)  # 128 x 64 tiles (plan target 128)
                 assert pl["bm"] == (128 if tiles128 >= 128 else 64), pl
+                # K groups (round 5): 64-row tiles whose 9 Cin / k-step steps split into an
+                # even number of 3-step super-steps
+                ksteps = 9 * cin // (32 if split else 64)
+                kg = win in ("2", "3") and pl["bm"] == 64 and ksteps % 6 == 0
+                assert pl["nw"] == (8 if kg else 4), pl
+                if kg:
+                    assert (pl["k_per_split"] // (32 if split else 64)) % 6 == 0, pl
             out = ops.conv2d(prec, xin.cuda(), wp, cout, 3, 3, 1, 1, bias=b.cuda(), act="relu",
                              residual=rin.cuda() if res else None)
             torch.cuda.synchronize()

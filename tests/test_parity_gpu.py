@@ -113,6 +113,29 @@ def test_resnet18_fp16m_c2_seeds(spi, zoo, gpu, seed):
     assert top1_agreement(got, ref) == 1.0
 
 
+@pytest.mark.parametrize("win", ["2", "3"])
+def test_resnet18_fp16m_window_kgroups(spi, zoo, gpu, win, monkeypatch):
+    """C2 with the layer-2..4 3x3 convs on the window kind's two-K-group (8-wave) tiles
+    (SPI_GEMM_WIN=2: the 4-wave plan's split-K slices, 3: half of them)."""
+    m = zoo.resnet18()
+    x = image(np.random.default_rng(5), 8, 224)
+    ref = cpu_inference(m, [x])[0]
+    monkeypatch.setenv("SPI_GEMM_WIN", win)
+    spi.lib.spi_debug_gemm_reload_env()
+    try:
+        rep = spi.ModelReplica(m, 0, "fp16m", max_batch=8)
+        got = hip_forward(spi, rep, [x], ref.shape)
+        got_g = hip_forward(spi, rep, [x], ref.shape, graphs=True)
+    finally:
+        monkeypatch.delenv("SPI_GEMM_WIN")
+        spi.lib.spi_debug_gemm_reload_env()
+    err = normalized_max_error(got, ref)
+    print(f"resnet18@224 bs8 fp16m win={win} err={err:.3e}")
+    assert err < TOL_RESNET18_FP16M
+    assert top1_agreement(got, ref) == 1.0
+    np.testing.assert_array_equal(got, got_g)
+
+
 def bert_inputs(rng, b, s, vocab=30522, pad_from=None):
     ids = rng.integers(0, vocab, size=(b, s), dtype=np.int64)
     mask = np.ones((b, s), dtype=np.int64)
