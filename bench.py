@@ -529,6 +529,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=5,
                     help="re-time the same K-step region this many times after `value` (value_repeats)")
     ap.add_argument("--graphs", type=int, default=1, help="capture the forward body into hipGraphs")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0: 2 x workers + 8, at least the environment's)")
     ap.add_argument("--cpu-seconds", type=float, default=9.0, help="CPU baseline budget over its layouts (0 = skip)")
     ap.add_argument("--e2e-requests", type=int, default=4000)
     ap.add_argument("--extras", type=int, default=1, help="extra measurements (0 = skip)")
@@ -558,7 +560,7 @@ def main():
     # run serially -- 28.4k -> 38.1k inf/s at 4 workers going from 4 to 8 queues.  Room for the
     # harness's worker streams plus the runtime's workers and copy stream.  Must be set before the
     # first HIP call.
-    queues = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 2 * args.workers + 8))
+    queues = min(32, args.hw_queues or max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 2 * args.workers + 8))
     os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
 
     rank = int(os.environ.get("RANK", "0"))
