@@ -1055,7 +1055,7 @@ void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStrea
                                        (double)B * 3 * image_ * image_ * 4 + (double)B * PH * PH * stem_.cout * (split_ ? 4 : 2));
     for (int r = 0; r < nrep; ++r)
       stem_pool(static_cast<const float*>(in[0]), ptr<void>(stem_pool_w_), ptr<float>(stem_.b), w.bufs[2], B, image_,
-                image_, stem_.prec != Prec::F16, split_, stem_pr_, s);
+                image_, split_ ? 2 : stem_.prec != Prec::F16 ? 1 : 0, split_, stem_pr_, s);
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_RESNET) {
     const int nrep = !prof_ ? 1 : op_begin(s, "ingest_nchw", 0, (double)B * 3 * image_ * image_ * 4 * 2);

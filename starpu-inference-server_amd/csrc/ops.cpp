@@ -193,7 +193,7 @@ int spi_op_stem_pool(int32_t precision, const float* x, int32_t B, int32_t H, in
       rows_per_block < 0 || rows_per_block > 2)
     return fail("invalid stem_pool arguments");
   if ((W + 6 - 7) / 2 + 1 > spi::kStemPoolMaxOW) return fail("stem_pool: image wider than 224");
-  spi::stem_pool(x, Wp, bias, y, B, H, W, precision >= 2, precision == 3, rows_per_block,
+  spi::stem_pool(x, Wp, bias, y, B, H, W, precision >= 2 ? 2 : 0, precision == 3, rows_per_block,
                  static_cast<hipStream_t>(stream));
   return check_launch();
 }

@@ -170,7 +170,9 @@ void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,
 constexpr int kStemPoolMaxOW = 112;  // stem output width bound (images up to 224)
 constexpr size_t stem_pool_bytes() { return (size_t)2 * 64 * 24 * 8 * sizeof(_Float16); }
 void stem_pool_pack(const float* w_folded /* [64][3][7][7] */, _Float16* dst);
-void stem_pool(const float* x, const void* w, const float* bias, void* y, int B, int H, int W, bool lo,
+// lo: 0 fp16 weights, 1 hi + lo weights on the fp16 image (fp16m), 2 hi + lo weights on the split
+// image (fp16x3; required for the split output)
+void stem_pool(const float* x, const void* w, const float* bias, void* y, int B, int H, int W, int lo,
                bool split, int pr, hipStream_t s);
 // 3x3/s2/p1 max pool on NHWC.
 void maxpool_nhwc(const void* x, void* y, int B, int H, int W, int C, int OH,

@@ -76,7 +76,11 @@ __device__ __forceinline__ half8 window(const u32x8& b) {
 }
 
 // OUT 0: fp16 NHWC [B][PH][PW][64]; 1: split NHWC (per pixel [32 hi | 32 lo] x 2).
-template <int PR, int NW, bool LO, int OUT>
+// LOM 0: fp16 image x fp16 weights (one MFMA per fragment pair); 1: fp16 image x hi + lo weights
+// (two: fp16m, round 5 -- the image's own fp16 rounding costs C2 0.03e-3 of parity margin,
+// tools/prec_emulate.py, and its lo planes + third MFMA a third of the launch); 2: split image x
+// split weights (three: fp16x3, fp32-grade).
+template <int PR, int NW, int LOM, int OUT>
 __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restrict__ x, const _Float16* __restrict__ w,
                                                             const float* __restrict__ bias, void* __restrict__ y, int H,
                                                             int W, int OH, int OW, int PH, int PW, int diag) {
@@ -84,6 +88,8 @@ __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restr
   constexpr int R = G::R, NR = G::NR, WP = G::WP, NPL = G::NPL, PD = G::PD, NT = 64 * NW;
   static_assert(NW == 4 || NW == 8, "4 waves (one per 16 channels), or 8 (x 2 pixel groups)");
   static_assert(NW == 4 || kStemPoolMaxOW <= 128, "8 waves: one 64-pixel group per wave");
+  constexpr bool LO = LOM == 2;   // lo image planes
+  constexpr bool WLO = LOM >= 1;  // lo weights
   // images: [copy 0 hi | copy 1 hi | copy 0 lo | copy 1 lo], copy 1 = copy 0 shifted one dword
   __shared__ __attribute__((aligned(16))) unsigned lds[(LO ? 4 : 2) * PD];
   __shared__ float xch[NW == 8 ? 2 * PR * kCout : 1];  // 8 waves: group 0's last column per pooled row
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restr
   for (int s = 0; s < kSteps; ++s) {
     const _Float16* src = w + ((size_t)n * kGroups + 4 * s + fq) * 8;
     wh[s] = *reinterpret_cast<const half8*>(src);
-    if constexpr (LO) wl[s] = *reinterpret_cast<const half8*>(src + kCout * kGroups * 8);
+    if constexpr (WLO) wl[s] = *reinterpret_cast<const half8*>(src + kCout * kGroups * 8);
   }
   const float bn = bias[n];
   if (diag == 3) return;  // diagnostic (SPI_STEM_DIAG): empty launch
@@ -210,8 +216,8 @@ __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restr
         if constexpr (LO) {
           const half8 al = window<P>(bb[2 + (P & 1)]);
           acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh[s], acc[P], 0, 0, 0);
-          acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl[s], acc[P], 0, 0, 0);
         }
+        if constexpr (WLO) acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl[s], acc[P], 0, 0, 0);
         acc[P] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh[s], acc[P], 0, 0, 0);
       };
       mma(std::integral_constant<int, 0>{});
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(64 * NW) void stem_pool_kernel(const float* __restr
 
 template <int PR, int NW>
 void launch_pr(const float* x, const _Float16* w, const float* bias, void* y, int B, int H, int W, int OH, int OW,
-               int PH, int PW, bool lo, bool split, hipStream_t s) {
+               int PH, int PW, int lo, bool split, hipStream_t s) {
   // diagnostic builds only (-DSPI_STEM_DIAG=1: no image loads, 2: fill only, 3: empty)
 #ifdef SPI_STEM_DIAG
   constexpr int diag = SPI_STEM_DIAG;
@@ -304,11 +310,13 @@ void launch_pr(const float* x, const _Float16* w, const float* bias, void* y, in
 #endif
   const dim3 grid((PH + PR - 1) / PR, B), block(64 * NW);
   if (split)
-    SPI_LAUNCH((stem_pool_kernel<PR, NW, true, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
-  else if (lo)
-    SPI_LAUNCH((stem_pool_kernel<PR, NW, true, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, 2, 1>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+  else if (lo == 2)
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, 2, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+  else if (lo == 1)
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, 1, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
   else
-    SPI_LAUNCH((stem_pool_kernel<PR, NW, false, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
+    SPI_LAUNCH((stem_pool_kernel<PR, NW, 0, 0>), grid, block, 0, s, x, w, bias, y, H, W, OH, OW, PH, PW, diag);
 }
 
 }  // namespace
@@ -326,12 +334,13 @@ void stem_pool_pack(const float* w, _Float16* dst) {
       }
 }
 
-void stem_pool(const float* x, const void* w, const float* bias, void* y, int B, int H, int W, bool lo, bool split,
+void stem_pool(const float* x, const void* w, const float* bias, void* y, int B, int H, int W, int lo, bool split,
                int pr, hipStream_t s) {
   const int OH = (H + 6 - 7) / 2 + 1, OW = (W + 6 - 7) / 2 + 1;
   const int PH = (OH + 2 - 3) / 2 + 1, PW = (OW + 2 - 3) / 2 + 1;
   if (OW > kStemPoolMaxOW || OH < 1 || OW < 1 || B < 1) throw std::runtime_error("stem_pool: unsupported image size");
-  if (split && !lo) throw std::runtime_error("stem_pool: split output needs split weights");
+  if (split && lo != 2) throw std::runtime_error("stem_pool: split output needs the split image and weights");
+  if (lo < 0 || lo > 2) throw std::runtime_error("stem_pool: lo is 0, 1 or 2");
   const _Float16* wp = static_cast<const _Float16*>(w);
   // pr: 1 / 2 pooled rows per 4-wave workgroup; 0 (default): two rows per 8-wave
   // workgroup (one 64-pixel group per wave) when the map has two groups, else 1 x 4 waves
