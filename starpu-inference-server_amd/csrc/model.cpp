@@ -1114,28 +1114,26 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         int ident = cur;
         if (b.has_ds) {  // the downsample reads the block input too: grouped with conv1
           ident = pick({cur, t1});
-          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, b.ds, buf[ident], mixed_, w, s);
+          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, b.ds, buf[ident], false, w, s);
         } else {
           run_conv(b.c1, buf[cur], B, H, H, buf[t1], OH, OW, Act::Relu, nullptr, w, s);
         }
         const int t2 = pick({cur, t1, ident});
         run_conv(b.c2, buf[t1], B, H, H, buf[t2], H2, OW, Act::Relu, nullptr, w, s);
         const int o = pick({cur, t2, ident});
-        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
-                 mixed_ && b.has_ds);
+        run_conv(b.c3, buf[t2], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
         cur = o;
       } else {
         const int t1 = pick({cur});
         int ident = cur;
-        if (b.has_ds) {  // F16M: hi + lo weights, fp32 out (the next conv's fp32 residual)
+        if (b.has_ds) {  // F16M: hi + lo weights, fp16 out like every conv (round 5: fp32 out kept nothing)
           ident = pick({cur, t1});
-          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, b.ds, buf[ident], mixed_, w, s);
+          run_conv_pair(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, b.ds, buf[ident], false, w, s);
         } else {
           run_conv(b.c1, buf[cur], B, H, H, buf[t1], H2, OW, Act::Relu, nullptr, w, s);
         }
         const int o = pick({cur, t1, ident});
-        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s, false,
-                 mixed_ && b.has_ds);
+        run_conv(b.c2, buf[t1], B, H2, H2, buf[o], OH, OW, Act::Relu, buf[ident], w, s);
         cur = o;
       }
       H = H2;
