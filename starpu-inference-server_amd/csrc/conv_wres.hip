@@ -344,8 +344,12 @@ int env_int(const char* name, int dflt) {
   return e && *e ? std::atoi(e) : dflt;
 }
 
-// SPI_CONV_WRES=0: never route here (A/B runs).  Read once; conv_wres_reload_env()
-// (spi_debug_gemm_reload_env) re-reads it.
+// SPI_CONV_WRES=0: never route here; 1 (default): only grids the implicit GEMM cannot fill,
+// fewer than kWresMaxTiles 128-row tiles; 2: every eligible conv (the round-3..4 rule).  Round 5,
+// under the four worker streams: since the kw-window kind (round 4) the implicit
+// GEMM beats this kernel at ResNet-18 bs8 (+1.9 % fp16m, +2.2 % fp16) and ResNet-152 bs32 (+2.4 %),
+// ties at ResNet-152 bs8, and loses at ResNet-18 bs1 (-3.9 %).  Read once;
+// conv_wres_reload_env() (spi_debug_gemm_reload_env) re-reads it.
 int& wres_on() {
   static int on = env_int("SPI_CONV_WRES", 1);
   return on;
@@ -368,8 +372,11 @@ static int wres_rows(int H, int W) {
   return th;
 }
 
+constexpr int kWresMaxTiles = 128;  // the general kernel's plan target
+
 bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p) {
   const int on = wres_on();
+  if (on == 1 && (d.M + 127) / 128 >= kWresMaxTiles) return false;  // a full 128 x 64 window grid
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   return on && prec == Prec::F16 && d.conv && d.KH == 3 && d.KW == 3 && d.stride == 1 && d.pad == 1 &&
          d.Cin == 64 && d.N == 64 && d.K == 576 && d.Kpad == 576 && d.krep == 1 && d.OH == d.H && d.OW == d.W &&

@@ -499,7 +499,15 @@ def test_conv3x3_c64_weight_resident(ops, B, H, res, act, bias):
     if act == "relu":
         ref = F.relu(ref)
     wp = ops.pack_weight("fp16", ops.conv_weight_matrix(w, 64))
-    out = ops.conv2d("fp16", x.cuda(), wp, 64, 3, 3, 1, 1, bias=b.cuda() if bias else None,
-                     residual=r.cuda() if res else None, act=act)
+    import os
+    try:  # every eligible conv (the default keeps the kernel for grids under 128 row tiles)
+        os.environ["SPI_CONV_WRES"] = "2"
+        ops.lib.spi_debug_gemm_reload_env()
+        out = ops.conv2d("fp16", x.cuda(), wp, 64, 3, 3, 1, 1, bias=b.cuda() if bias else None,
+                         residual=r.cuda() if res else None, act=act)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("SPI_CONV_WRES", None)
+        ops.lib.spi_debug_gemm_reload_env()
     err = normalized_max_error(out.float().cpu().numpy(), ref.numpy())
     assert err < 2e-3, f"wres conv B{B} H{H} res={res} act={act}: {err:.3e}"
