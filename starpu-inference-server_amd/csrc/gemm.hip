@@ -1703,7 +1703,10 @@ struct Knobs {
 constexpr int kHaloStages = 3;     // W ring of the halo kinds
 constexpr int kHaloMinH = 14;      // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 constexpr int kHaloMaxTiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles
-constexpr int kSt3Min = 16, kSt4Min = 32;  // ring depth by k-steps per slice (4 stages: BERT FFN2 +2.4 %)
+#ifndef SPI_ST3_MIN  // variant builds (tools/build_variant.sh ... -DSPI_ST3_MIN=N) for ring-depth A/Bs
+#define SPI_ST3_MIN 16
+#endif
+constexpr int kSt3Min = SPI_ST3_MIN, kSt4Min = 32;  // ring depth by k-steps per slice (4 stages: BERT FFN2 +2.4 %)
 
 Knobs read_knobs() {
   Knobs k;
@@ -2121,7 +2124,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
     const int sp = std::max(1, std::min({(T0 + t64 - 1) / t64, ksteps / 6, q0.splits}));
     if (sp < q0.splits) {
       const int kt = (ksteps + sp - 1) / sp;
-      q0 = finish_plan(Plan{64, 64, kt >= 16 ? 3 : 2, sp, 0}, ksteps, ES, d0.krep);
+      q0 = finish_plan(Plan{64, 64, kt >= kSt3Min ? 3 : 2, sp, 0}, ksteps, ES, d0.krep);
       if (q1.splits == 1) q1.stages = q0.stages;
     }
   }
@@ -2132,7 +2135,7 @@ void launch_pair(const GemmDesc& d0, const GemmPtrs& p0, const GemmDesc& d1, con
     const auto t = [](const GemmDesc& d, int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
     if (t(d0, 128, 64) + t(d1, 128, 64) >= knobs().target) {
       const int ES = estep_of(pr), k0 = d0.Kpad / ES, k1 = d1.Kpad / ES;
-      const int st = std::max(k0, k1) >= 16 ? 3 : 2;
+      const int st = std::max(k0, k1) >= kSt3Min ? 3 : 2;
       q0 = finish_plan(Plan{128, 64, st, 1, 0}, k0, ES, d0.krep);
       q1 = finish_plan(Plan{128, 64, st, 1, 0}, k1, ES, d1.krep);
     }
