@@ -376,7 +376,10 @@ void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S,
                int hd, float scale, bool f16, hipStream_t s) {
   if (hd != HD) return;  // validated at model build time
   const dim3 grid((S + QT - 1) / QT, B * heads);
-  if (f16 && S > 128) {
+#ifndef SPI_ATTN_S8_MIN  // variant builds: the 8-wave kernel from this sequence length on
+#define SPI_ATTN_S8_MIN 129
+#endif
+  if (f16 && S >= SPI_ATTN_S8_MIN) {
     const dim3 g8((S + 127) / 128, B * heads);
     SPI_LAUNCH(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
