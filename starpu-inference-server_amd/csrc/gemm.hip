@@ -1929,7 +1929,12 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
   // a deeper ring pays only on long K loops (4 stages only reach the 64x64 tiles, finish_plan caps the others)
   const auto stages_for = [](int kt) { return kt >= kSt4Min ? 4 : kt >= kSt3Min ? 3 : 2; };
-  if (d.pool_rows) return finish_plan(Plan{64, 64, stages_for(ksteps), 1, 0}, ksteps, ES, d.krep);  // one image per tile row
+#ifndef SPI_FC_SPLITS  // variant builds: split-K slices of the pooled FC (avgpool + FC in one GEMM)
+#define SPI_FC_SPLITS 1
+#endif
+  if (d.pool_rows)  // one image per tile row
+    return finish_plan(Plan{64, 64, stages_for((ksteps + SPI_FC_SPLITS - 1) / SPI_FC_SPLITS), SPI_FC_SPLITS, 0}, ksteps,
+                       ES, d.krep);
   if (Plan h = halo_plan(d, prec, k.target); h.halo) return h;
   const int T = k.target;
   if (d.N > 64 && tiles_of(128, 128) >= T) return finish_plan(Plan{128, 128, 2, 1, 0}, ksteps, ES, d.krep);

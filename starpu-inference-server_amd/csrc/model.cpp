@@ -922,12 +922,19 @@ void Model::run_qkv_attention(const LinearW& L, const void* x, const float* in_s
 // is the A operand as is, so the pooled vector never goes through HBM.
 bool Model::pooled_fc(int hw) const { return hw > 0 && hw <= 64 && (!split_ || feat_ % 32 == 0); }
 
-void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s) {
+GemmDesc Model::pooled_fc_desc(int B, int hw) const {
   GemmDesc d = linear_desc(fc_, B * hw, feat_, classes_);
   d.pool_rows = hw;
   d.out_f32 = true;
   d.a_split = split_;
   d.wplane = fc_.wplane;
+  return d;
+}
+
+void Model::run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s) {
+  const GemmDesc d = pooled_fc_desc(B, hw);
+  if (gemm_partial_floats(d, fc_.prec) > ws.partial_floats || gemm_counter_slots(d, fc_.prec) > kCounterSlots)
+    throw std::runtime_error("split-K workspace too small");
   const size_t es = f16_ ? 2 : 4;
   const int nrep = !prof_ ? 1 : op_begin(s, "avgpool_fc_M" + std::to_string(B * hw) + "_N" + std::to_string(classes_) + "_K" +
                     std::to_string(feat_),
@@ -996,6 +1003,7 @@ Workspace* Model::workspace(hipStream_t s) {
       H = H2;
     }
     partial = std::max(partial, linear_partial(fc_, B));
+    if (pooled_fc(H * H)) partial = std::max(partial, gemm_partial_floats(pooled_fc_desc(B, H * H), fc_.prec));
     for (int i = 0; i < 5; ++i) sizes.push_back(amax * ea);
     sizes.push_back((size_t)B * feat_ * ea);  // pooled (fp32 under F16M: the FC's A)
   } else if (family_ == SPI_FAMILY_BERT) {

@@ -147,6 +147,7 @@ class Model {
   void run_pooled_fc(const void* act, int B, int hw, void* out, Workspace& ws, hipStream_t s);
   size_t conv_partial(const ConvW& c, int B, int H, int W) const;
   size_t linear_partial(const LinearW& L, int M) const;
+  GemmDesc pooled_fc_desc(int B, int hw) const;  // avgpool + FC as one GEMM (pool_rows = hw)
   template <typename P>
   const P* ptr(size_t off) const {
     return reinterpret_cast<const P*>(static_cast<const char*>(dblob_) + off);
