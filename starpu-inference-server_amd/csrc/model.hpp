@@ -176,7 +176,10 @@ class Model {
   std::vector<int> stage_blocks_;
   ConvW stem_;
   bool stem_fused_ = false;  // stem + max pool in one launch on the NCHW input (stem.hip)
-  int stem_pr_ = 0;          // its workgroup shape (0 = auto, stem.hip)
+#ifndef SPI_STEM_PR  // variant builds: 1 / 2 pooled rows per 4-wave workgroup (stem.hip)
+#define SPI_STEM_PR 0
+#endif
+  int stem_pr_ = SPI_STEM_PR;  // its workgroup shape (0 = auto, stem.hip)
   size_t stem_pool_w_ = 0;   // its weights, [hi | lo][64][24][8] fp16
   std::vector<ResBlock> blocks_;
   LinearW fc_;
