@@ -450,7 +450,10 @@ void Model::build_resnet(const PMap& p) {
       blocks_.push_back(blk);
     }
   }
-  fc_ = pack_linear_named(p, "fc", prec_, mixed_);
+#ifndef SPI_FC_HILO  // variant builds: 0 = the fp16m FC on plain fp16 weights
+#define SPI_FC_HILO 1
+#endif
+  fc_ = pack_linear_named(p, "fc", prec_, mixed_ && SPI_FC_HILO);
   classes_ = fc_.n;
   feat_ = fc_.k;
   // Channel chain: every conv must read exactly the channels its producer
