@@ -450,8 +450,10 @@ void Model::build_resnet(const PMap& p) {
       blocks_.push_back(blk);
     }
   }
-#ifndef SPI_FC_HILO  // variant builds: 0 = the fp16m FC on plain fp16 weights
-#define SPI_FC_HILO 1
+  // F16M: plain fp16 FC weights since round 5 (hi + lo kept the logits 0.06e-3 closer on 8 emulated
+  // seeds and cost 1 % of C2); define SPI_FC_HILO=1 for the hi + lo packing
+#ifndef SPI_FC_HILO
+#define SPI_FC_HILO 0
 #endif
   fc_ = pack_linear_named(p, "fc", prec_, mixed_ && SPI_FC_HILO);
   classes_ = fc_.n;
