@@ -1,9 +1,11 @@
 // HBM-bound kernels around the MFMA contractions (gfx950): layout ingest,
 // pooling, LayerNorm, BERT embedding gather + LN, ViT patchify/assembly.
 // All loads/stores are 16-byte vectors where the layout allows (G13).
+#include "ln_fold.hpp"
 #include "spi_kernels.hpp"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace spi {
 namespace {
@@ -266,6 +268,27 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int ldx,
                  yt ? yt + (size_t)row * ldy : nullptr, lane);
 }
 
+// LayerNorm of rows held in two fp16 planes (GemmDesc::res_planes: x = hi + lo, lo `plane`
+// elements after hi) -- ViT's final class-token LayerNorm over the two-plane residual stream.
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_planes_kernel(const _Float16* xh, size_t plane, int ldx,
+                                                               const float* g, const float* b, float* yf, T* yt,
+                                                               int ldy, int rows, int D, float eps) {
+  constexpr int VPL = 16;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const _Float16* xr = xh + (size_t)row * ldx;
+  float v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < D ? static_cast<float>(xr[c]) + static_cast<float>(xr[c + plane]) : 0.f;
+  }
+  ln_row<T, VPL>(v, D, g, b, eps, yf ? yf + (size_t)row * ldy : nullptr, yt ? yt + (size_t)row * ldy : nullptr,
+                 lane);
+}
+
 // LayerNorm rows of D = NV * 256: one wave per row, every lane holds NV float4
 // column groups (c = 4 * (64 j + lane)), so the row moves as 16-byte loads and
 // stores (fp16 copies as 8-byte stores) -- a quarter of the scalar kernel's
@@ -394,6 +417,46 @@ __global__ void vit_assemble_kernel(const float* __restrict__ patches,
   }
 }
 
+// ViT stream assembly into the two-plane residual stream (GemmDesc::res_planes) plus the rows'
+// per-64-column chunk statistics (ln_fold.hpp) that the first layer's folded QKV GEMM reads: one
+// thread per 8 columns of a row, 8 consecutive threads = one 64-column chunk (D % 64 == 0, so a
+// chunk never straddles rows or 8-lane groups); 16-byte loads and stores.
+__global__ __launch_bounds__(256) void vit_assemble_planes_kernel(const float* __restrict__ patches,
+                                                                  const float* __restrict__ cls,
+                                                                  const float* __restrict__ pos,
+                                                                  _Float16* __restrict__ xh, size_t plane,
+                                                                  float* __restrict__ stats, int B, int P, int D) {
+  typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+  const int groups = D >> 3;
+  const size_t n = (size_t)B * (P + 1) * groups;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // every lane of an 8-lane group takes part in the chunk shuffles: past the end, repeat the last
+  // group (n is a multiple of 8) and store nothing
+  const size_t gi = gid < n ? gid : n - 1;
+  const size_t r = gi / groups;
+  const int c0 = (int)(gi - r * groups) * 8;
+  const int t = (int)(r % (P + 1)), b = (int)(r / (P + 1));
+  const float* src = t == 0 ? cls + c0 : patches + ((size_t)b * P + (t - 1)) * D + c0;
+  const float* pp = pos + (size_t)t * D + c0;
+  const float4 s0 = reinterpret_cast<const float4*>(src)[0], s1 = reinterpret_cast<const float4*>(src)[1];
+  const float4 p0 = reinterpret_cast<const float4*>(pp)[0], p1 = reinterpret_cast<const float4*>(pp)[1];
+  const float y[8] = {s0.x + p0.x, s0.y + p0.y, s0.z + p0.z, s0.w + p0.w,
+                      s1.x + p1.x, s1.y + p1.y, s1.z + p1.z, s1.w + p1.w};
+  float mean, m2;
+  ln_chunk_stats(y, mean, m2);
+  if (gid >= n) return;
+  half8 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hi[e] = static_cast<_Float16>(y[e]);
+    lo[e] = static_cast<_Float16>(y[e] - static_cast<float>(hi[e]));
+  }
+  _Float16* xr = xh + r * D + c0;
+  *reinterpret_cast<half8*>(xr) = hi;
+  *reinterpret_cast<half8*>(xr + plane) = lo;
+  if (stats && (c0 & 63) == 0) reinterpret_cast<float2*>(stats)[r * (D >> 6) + (c0 >> 6)] = float2{mean, m2};
+}
+
 template <typename T>
 __global__ void gather_rows_kernel(const float* __restrict__ x, T* __restrict__ y, int rows,
                                    int stride_rows, int D) {
@@ -520,6 +583,26 @@ void vit_assemble(const float* patches, const float* cls, const float* pos, floa
   const size_t n = (size_t)B * (P + 1) * D;
   SPI_LAUNCH(vit_assemble_kernel, dim3(grid_for(n)), dim3(256), 0, s, patches, cls,
                      pos, x, B, P, D);
+}
+
+void vit_assemble_planes(const float* patches, const float* cls, const float* pos, _Float16* xh, size_t plane,
+                         float* stats, int B, int P, int D, hipStream_t s) {
+  if (D % 64 || plane % 8) throw std::invalid_argument("vit_assemble_planes: D % 64 == 0, plane % 8 == 0");
+  const size_t n = (size_t)B * (P + 1) * (D / 8);
+  SPI_LAUNCH(vit_assemble_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, patches, cls, pos, xh,
+             plane, stats, B, P, D);
+}
+
+void layernorm_planes(const _Float16* xh, size_t plane, int ldx, const float* g, const float* b, float* yf, void* yt,
+                      int ldy, int rows, int D, float eps, bool f16, hipStream_t s) {
+  if (D > 1024) throw std::invalid_argument("layernorm_planes: D <= 1024");
+  const dim3 grid((rows + 3) / 4);
+  if (f16)
+    SPI_LAUNCH((layernorm_planes_kernel<_Float16>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf, (_Float16*)yt,
+               ldy, rows, D, eps);
+  else
+    SPI_LAUNCH((layernorm_planes_kernel<float>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf, (float*)yt, ldy,
+               rows, D, eps);
 }
 
 void gather_rows(const float* x, void* y, int rows, int stride_rows, int D, bool f16,

@@ -248,6 +248,10 @@ __device__ __forceinline__ float load_res(const KArgs& a, int m, int n) {
     return static_cast<float>(R[i]) + static_cast<float>(R[i + 32]);
   }
   const size_t idx = (size_t)m * a.d.ldr + n;
+  if (a.d.res_planes) {  // two fp16 planes: hi + lo
+    const _Float16* R = static_cast<const _Float16*>(a.p.res);
+    return static_cast<float>(R[idx]) + static_cast<float>(R[idx + a.d.plane]);
+  }
   return a.d.res_f32 ? static_cast<const float*>(a.p.res)[idx]
                      : static_cast<float>(static_cast<const Out*>(a.p.res)[idx]);
 }
@@ -822,7 +826,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
   constexpr bool RPF = BM == 64 && BN == 64 && !HALO && NW == 4;
   // the LayerNorm fold lives in the dense fp16 instances only (the transformer GEMMs)
   constexpr bool LNF = KIND == kDense && MODE == (int)Prec::F16;
-  [[maybe_unused]] const int res_rb = (MODE == kF16X3S || sizeof(typename TR::Out) == 4 || d.res_f32) ? 256 : 128;
+  // (residual planes: a row's 64 hi values, then its 64 lo values)
+  [[maybe_unused]] const int res_rb =
+      (MODE == kF16X3S || sizeof(typename TR::Out) == 4 || d.res_f32 || d.res_planes) ? 256 : 128;
   [[maybe_unused]] const int rpw = res_rb * BM / 1024 / NW;  // 2 or 4
   [[maybe_unused]] const bool rpf_tile = RPF && a.p.res && a.vec_ok && n0 + BN <= d.N && !d.pool_rows;
   // (window kind: into the window buffer the last super-step does not use -- 9 KiB, so fp16
@@ -844,6 +850,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           if (m < m_lim) {
             if constexpr (MODE == kF16X3S)
               src = reinterpret_cast<const char*>(static_cast<const _Float16*>(a.p.res) + split_idx(m, n0, d.ldr)) + ch * 16;
+            else if (d.res_planes)
+              src = reinterpret_cast<const char*>(static_cast<const _Float16*>(a.p.res) + (size_t)m * d.ldr + n0 +
+                                                  (ch >= 8 ? d.plane : 0)) + (ch & 7) * 16;
             else
               src = static_cast<const char*>(a.p.res) + ((size_t)m * d.ldr + n0) * (res_rb / 64) + ch * 16;
           }
@@ -935,7 +944,9 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
     constexpr int G = BN / 8, RSTEP = NT / G, ITEMS = BM / RSTEP;
     const int cg = tid % G, r0 = tid / G;
     const int nb = n0 + cg * 8;
-    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : d.out_f16 ? 0 : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
+    // 0 fp16, 1 fp32, 2 split layout, 3 two fp16 planes
+    const int fmt = (kSplitMode<MODE> && d.out_split) ? 2 : d.out_planes ? 3 : d.out_f16 ? 0
+                    : (d.out_f32 || sizeof(Out) == 4) ? 1 : 0;
     // output row of tile row `row`, -1 when it is not stored
     auto row_m = [&](int row) -> int {
       if constexpr (HALO) {
@@ -1031,6 +1042,11 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
               const half8 lo = *reinterpret_cast<const half8*>(q + 64);
 #pragma unroll
               for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
+            } else if (d.res_planes) {
+              const half8 hi = *reinterpret_cast<const half8*>(rr + cg * 16);
+              const half8 lo = *reinterpret_cast<const half8*>(rr + 128 + cg * 16);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
             } else if (d.res_f32 || sizeof(Out) == 4) {
               const floatx4 r0v = *reinterpret_cast<const floatx4*>(rr + cg * 32);
               const floatx4 r1v = *reinterpret_cast<const floatx4*>(rr + cg * 32 + 16);
@@ -1054,6 +1070,12 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
               const _Float16* R = static_cast<const _Float16*>(a.p.res) + split_idx(m, nb, d.ldr);
               const half8 hi = *reinterpret_cast<const half8*>(R);
               const half8 lo = *reinterpret_cast<const half8*>(R + 32);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
+            } else if (d.res_planes) {
+              const _Float16* R = static_cast<const _Float16*>(a.p.res) + (size_t)m * d.ldr + nb;
+              const half8 hi = *reinterpret_cast<const half8*>(R);
+              const half8 lo = *reinterpret_cast<const half8*>(R + d.plane);
 #pragma unroll
               for (int e = 0; e < 8; ++e) y[it][e] = static_cast<float>(hi[e]) + static_cast<float>(lo[e]);
             } else if (d.res_f32 || sizeof(Out) == 4) {
@@ -1109,10 +1131,12 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
               if (m < 0) continue;
               if ((cg & 7) == 0)
                 reinterpret_cast<float2*>(a.p.ln.out_stats)[(size_t)m * (d.N >> 6) + (nb >> 6)] = float2{mean, m2};
-              half8 h;
+              if (a.p.ln.c16) {  // (two-plane outputs: the hi plane is the copy)
+                half8 h;
 #pragma unroll
-              for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(y[it][e]);
-              *reinterpret_cast<half8*>(a.p.ln.c16 + (size_t)m * d.ld16 + nb) = h;
+                for (int e = 0; e < 8; ++e) h[e] = static_cast<_Float16>(y[it][e]);
+                *reinterpret_cast<half8*>(a.p.ln.c16 + (size_t)m * d.ld16 + nb) = h;
+              }
             }
           }
         }
@@ -1130,6 +1154,16 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
             _Float16* C = static_cast<_Float16*>(a.p.C) + split_idx(m, nb, d.ldc);
             *reinterpret_cast<half8*>(C) = hi;
             *reinterpret_cast<half8*>(C + 32) = lo;
+          } else if (fmt == 3) {
+            half8 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              hi[e] = static_cast<_Float16>(y[it][e]);
+              lo[e] = static_cast<_Float16>(y[it][e] - static_cast<float>(hi[e]));
+            }
+            _Float16* C = static_cast<_Float16*>(a.p.C) + (size_t)m * d.ldc + nb;
+            *reinterpret_cast<half8*>(C) = hi;
+            *reinterpret_cast<half8*>(C + d.plane) = lo;
           } else if (fmt == 1) {
             float* C = static_cast<float*>(a.p.C) + (size_t)m * d.ldc + nb;
             *reinterpret_cast<floatx4*>(C) = floatx4{y[it][0], y[it][1], y[it][2], y[it][3]};
@@ -1166,6 +1200,12 @@ __device__ __forceinline__ void gemm_body(const KArgs& a, const int kslice_in, c
           const _Float16 hi = static_cast<_Float16>(val);
           C[k] = hi;
           C[k + 32] = static_cast<_Float16>(val - static_cast<float>(hi));
+        } else if (fmt == 3) {
+          _Float16* C = static_cast<_Float16*>(a.p.C);
+          const size_t k = (size_t)m * d.ldc + n;
+          const _Float16 hi = static_cast<_Float16>(val);
+          C[k] = hi;
+          C[k + d.plane] = static_cast<_Float16>(val - static_cast<float>(hi));
         } else if (fmt == 1) {
           static_cast<float*>(a.p.C)[(size_t)m * d.ldc + n] = val;
         } else {
@@ -1690,6 +1730,11 @@ struct Knobs {
   // 1: none -- round 4 measured ViT-L FFN2 at 3 slices 100 -> 73 us back to back but C5 under the
   // four streams 6.05k -> 5.09k inf/s: the slices' CU-time and slab traffic cost the other streams more)
   int g256_split = 1;
+  // SPI_GEMM_256_ORDER: gemm256 tile order, 0 row blocks fastest, 1 column tiles fastest, -1 (default)
+  // by shape: column tiles fastest when A is the larger operand (M > N), so an XCD's consecutive
+  // workgroups share A row blocks (round 6, PMC FETCH_SIZE: ViT-L FFN2 142 -> 119 MB, out-proj
+  // 47.7 -> 41.9 MB; FFN1 (N = 4096) 61 -> 78 MB the other way; C5 four-stream +0.2 %)
+  int g256_order = -1;
   int halo_bm = 0;          // SPI_GEMM_HALO_CFG="rows,a|s": force a halo candidate (64 / 128 / 256 rows)
   bool halo_stacked = false;
   struct HaloPick {
@@ -1761,6 +1806,7 @@ Knobs read_knobs() {
       }
     }
   }
+  if (const char* e = std::getenv("SPI_GEMM_256_ORDER"); e && *e) k.g256_order = std::max(-1, std::min(1, std::atoi(e)));
   if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("SPI_GEMM_WIN"); e && *e) k.win = std::max(0, std::min(3, std::atoi(e)));
   return k;
@@ -2286,9 +2332,16 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
                     d.ldc % 8 == 0 && al16(p.C) && (!p.bias || al16(p.bias)) &&
                     (!p.res || (d.ldr % 8 == 0 && al16(p.res))) &&
                     (d.ln_in_chunks == 0 || (p.ln.in_stats && p.ln.c1 && al16(p.ln.c1))) &&
-                    (d.res_ln_chunks == 0 || (p.res && d.res_f32 && p.ln.res_stats && al16(p.ln.res_g) && al16(p.ln.res_b))) &&
-                    (!d.ln_out || (p.ln.out_stats && p.ln.c16 && al16(p.ln.c16) && d.ld16 % 8 == 0));
+                    (d.res_ln_chunks == 0 ||
+                     (p.res && (d.res_f32 || d.res_planes) && p.ln.res_stats && al16(p.ln.res_g) && al16(p.ln.res_b))) &&
+                    (!d.ln_out || (p.ln.out_stats && (p.ln.c16 ? al16(p.ln.c16) && d.ld16 % 8 == 0 : d.out_planes)));
     if (!ok) throw std::invalid_argument("LayerNorm fold: dense fp16 GEMM, N % 128 == 0, aligned vectors");
+  }
+  if (d.res_planes || d.out_planes) {
+    // two fp16 planes: the F16 dense epilogue, 16-byte aligned rows and plane offset
+    if (prec != Prec::F16 || d.conv || d.pool_rows || d.plane % 8 || (d.res_planes && (!p.res || d.res_f32)) ||
+        (d.out_planes && (d.out_f32 || d.out_f16)))
+      throw std::invalid_argument("two-plane residual / output: dense fp16 GEMM, plane offset a multiple of 8");
   }
   switch (prec) {
     case Prec::F16:
@@ -2296,7 +2349,8 @@ void gemm(const GemmDesc& d, const GemmPtrs& p, Prec prec, hipStream_t s) {
         conv_wres(d, p, s);
       else if (routes_256(d, prec) && (reinterpret_cast<uintptr_t>(p.A) & 15) == 0 &&
                (reinterpret_cast<uintptr_t>(p.W) & 15) == 0)  // 16-byte LDS-DMA pieces
-        gemm256(d, p, g256_splits(d), s, route_bm(d, prec), knobs().g128_nbuf);
+        gemm256(d, p, g256_splits(d), s, route_bm(d, prec), knobs().g128_nbuf,
+                knobs().g256_order >= 0 ? knobs().g256_order : d.M > d.N);
       else
         launch<(int)Prec::F16>(d, p, s);
       break;

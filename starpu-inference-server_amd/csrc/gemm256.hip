@@ -66,6 +66,10 @@ struct G256Args {
   int splits, ktp;
   float* partial;
   int* counters;
+  // tile order inside a slice: 0 row blocks fastest (consecutive tiles share a W panel), 1 column
+  // tiles fastest (consecutive tiles share an A row block; SPI_GEMM_256_ORDER)
+  int n_fast;
+  size_t plane;  // RES = 3: residual and output in two fp16 planes, lo `plane` elements after hi
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -121,8 +125,8 @@ __device__ __forceinline__ constexpr bool quarter_is_a(int q) {
   return BM == 128 ? q == 0 : (q == 0 || q == 3);
 }
 
-// RES: 0 no residual, 1 fp16 residual, 2 fp32 residual (a template parameter: the epilogue walk
-// stays branch-free).
+// RES: 0 no residual, 1 fp16 residual, 2 fp32 residual, 3 residual and output in two fp16 planes
+// (GemmDesc::res_planes / out_planes; a template parameter: the epilogue walk stays branch-free).
 // wait until at most N of this wave's LDS-DMA instructions are outstanding and its LDS
 // reads are done, then a workgroup barrier
 // (the s_waitcnt builtin, not inline asm: hipcc's waitcnt pass then knows the fragment
@@ -204,7 +208,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int slice = wgid / tiles, tile = wgid - slice * tiles;
-  const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
+  const int tm = g.n_fast ? tile / g.tiles_n : tile % g.tiles_m;
+  const int tn = g.n_fast ? tile - tm * g.tiles_n : tile / g.tiles_m;
   const int m0 = tm * BM, n0 = tn * 256;
   const int kt0 = slice * g.ktp;
   const int KT = min(g.ktp, (g.K >> 6) - kt0);
@@ -243,6 +248,72 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src[q][j] + kofs),
                                        (lds_ptr_t)(buf + dsto[q][j]), 16, 0, 0);
+  };
+
+  // LNC (the LayerNorm consumer fold, RES = 0, ln_in_chunks > 0): the tile rows' {mean, rstd}.
+  // Four lanes share a row: lane q of the four loads its 4 of the row's 16 chunk partials (two
+  // 16-byte loads) during the LAST k-tile (ln_load: 8 registers a round, once no DMA is left to
+  // issue), they land under its remaining MFMAs, and the epilogue combines them (ln_combine: Chan's
+  // formula over two xor-shuffle rounds).  Each thread loading its row's 16 partials in the epilogue
+  // (round 4) was a dependent memory round trip plus 32 live registers beside the 128 accumulators:
+  // 84 bytes of spills per lane, ViT-L FFN1 +8 us per launch with the fold (round 6,
+  // tools/loaded_ops.py).  Round h, half-wave lane l = tid & 31: row m0 + kRoundRows h + (tid >> 5)
+  // + 16 (l >> 2) -- the epilogue walk's pass l >> 2 -- chunks 4 (l & 3) .. + 3.
+  constexpr int kLnRounds = BM / Geo::kRoundRows;
+  [[maybe_unused]] floatx4 ln_ch[RES == 0 ? kLnRounds : 1][2];
+  [[maybe_unused]] float2 ln_st[RES == 0 ? kLnRounds : 1];
+  [[maybe_unused]] const bool lnc = RES == 0 && g.ln_in_chunks > 0;
+  auto ln_load = [&] {
+    if constexpr (RES == 0) {
+      if (lnc) {
+        const int q = tid & 3, pass = (tid & 31) >> 2;
+        // chunks past ln_in_chunks (D < 1024) re-read the row's last pair and are masked in ln_combine
+        const int c0 = min(4 * q, g.ln_in_chunks - 2), c1 = min(4 * q + 2, g.ln_in_chunks - 2);
+#pragma unroll
+        for (int h = 0; h < kLnRounds; ++h) {
+          const int m = min(m0 + Geo::kRoundRows * h + (tid >> 5) + 16 * pass, g.M - 1);
+          const float* p = g.ln_in_stats + (size_t)m * g.ln_in_chunks * 2;
+          ln_ch[h][0] = *reinterpret_cast<const floatx4*>(p + 2 * c0);
+          ln_ch[h][1] = *reinterpret_cast<const floatx4*>(p + 2 * c1);
+        }
+      }
+    }
+  };
+  auto ln_combine = [&] {
+    if constexpr (RES == 0) {
+      if (lnc) {
+        const int q = tid & 3;
+        const float k = (float)g.ln_in_chunks;
+#pragma unroll
+        for (int h = 0; h < kLnRounds; ++h) {
+          // this lane's chunks 4 q + j: (mean, M2) = ln_ch[h][j / 2] components 2 (j & 1), + 1
+          float mc[4], m2c[4];
+          bool ok[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const floatx4 v = ln_ch[h][j >> 1];
+            mc[j] = (j & 1) ? v[2] : v[0];
+            m2c[j] = (j & 1) ? v[3] : v[1];
+            ok[j] = 4 * q + j < g.ln_in_chunks;
+          }
+          float sm = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sm += ok[j] ? mc[j] : 0.f;
+          sm += __shfl_xor(sm, 1, 64);
+          sm += __shfl_xor(sm, 2, 64);
+          const float mean = sm / k;
+          float m2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float dm = mc[j] - mean;
+            m2 += ok[j] ? m2c[j] + 64.f * dm * dm : 0.f;
+          }
+          m2 += __shfl_xor(m2, 1, 64);
+          m2 += __shfl_xor(m2, 2, 64);
+          ln_st[h] = float2{mean, rsqrtf(m2 / (64.f * k) + g.ln_in_eps)};
+        }
+      }
+    }
   };
 
   floatx4 acc[kMA][4];
@@ -322,6 +393,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       bar();
       // phase 2
       read_a(buf, 1);
+      if constexpr (R == 0) ln_load();  // fa[0] is dead, nothing left to stage
       if constexpr (R >= 2) stage(0, kt + 2);
       bar();
       mma(1, 0);
@@ -341,23 +413,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     if (wr == 0) bar();  // the skew, closed
   } else if constexpr (NBUF == 3) {
     // 128 x 256: the same ping-pong of the two wave rows, 2 phases per k-tile, three buffers.
-    //   phase 0: reads A + B n-half 0 (T0, T1), stages T2 of tile t + 2, MFMAs (0, 0)
-    //   phase 1: reads B n-half 1 (T2),        stages T0 + T1 of tile t + 3, MFMAs (0, 1)
-    // The thirds go out in one sequence T0(0) T1(0) T2(0) T0(1) ... (the prologue issues the
-    // first 8); a region is restaged one phase after its last read (T2(t + 2) lands in the
-    // buffer of tile t - 1, whose T2 was read in the phase before; T0 / T1 (t + 3) in tile t's,
-    // read in phase 0), and every third has ~4 phases to land: 12 of a wave's pieces stay in
-    // flight at each wait (96 KiB per CU), never vmcnt(0) before the last k-tile.
+    //   phase 0: reads A + B n-half 0 (T0, T1), stages T0 + T1 of tile t + 2, MFMAs (0, 0)
+    //   phase 1: reads B n-half 1 (T2),        stages T2 of tile t + 2,      MFMAs (0, 1)
+    // Tile t + 2 goes into the buffer of tile t - 1, whose thirds wave row 0 read two phases
+    // earlier -- wave row 1 runs one barrier behind, so a region is restaged only after both
+    // rows' reads of it are done (round 6: the first schedule restaged one phase after row 0's
+    // read, racing row 1's).  The thirds go out in one sequence T0(0) T1(0) T2(0)
+    // T0(1) ... (the prologue issues tiles 0 and 1), each has ~4 phases to land.
     // With R = KT - 1 - t tiles after tile t, the waits after each phase's DMA:
-    //   phase 0 (T2(t) must have landed):      6 min(R, 2) pieces younger
-    //   phase 1 (T0, T1(t + 1) must have):     2 (1 + 3 [R >= 2] + 2 [R >= 3]); R = 0: none
-    const int npro = min(8, 3 * KT);
+    //   phase 0 (T2(t) must have landed):      2 (3 [R >= 1] + 2 [R >= 2]) pieces younger
+    //   phase 1 (T0, T1(t + 1) must have):     2 (1 + 3 [R >= 2]); R = 0: none
+    const int npro = min(6, 3 * KT);
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
+    for (int q = 0; q < 6; ++q)
       if (q < npro) stage(q % 3, q / 3);
-    if (KT >= 3)
-      vm_wait_nolgkm<12>();
-    else if (KT == 2)
+    if (KT >= 2)
       vm_wait_nolgkm<8>();
     else
       vm_wait_nolgkm<2>();
@@ -369,61 +439,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       // phase 0
       read_a(buf, 0);
       read_b(buf, 0);
-      if constexpr (R >= 2) stage(2, kt + 2);
-      vm_wait_nolgkm<6 * (R < 2 ? R : 2)>();
-      mma(0, 0);
-      bar();
-      // phase 1
-      read_b(buf, 1);
-      if constexpr (R >= 3) {
-        stage(0, kt + 3);
-        stage(1, kt + 3);
-      }
-      if constexpr (R >= 1)
-        vm_wait_nolgkm<2 * (1 + (R >= 2 ? 3 : 0) + (R >= 3 ? 2 : 0))>();
-      else
-        bar();
-      mma(0, 1);
-      bar();
-    };
-    for (int kt = 0; kt < KT - 3; ++kt) ktile(kt, std::integral_constant<int, 3>{});
-    if (KT > 2) ktile(KT - 3, std::integral_constant<int, 2>{});
-    if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
-    ktile(KT - 1, std::integral_constant<int, 0>{});
-    if (wr == 0) bar();  // the skew, closed
-  } else {
-    // 128 x 256 on two buffers (96 KiB: room for another kernel's 64 KiB workgroup on the CU).
-    //   phase 0: reads T0, T1, stages T2 of tile t + 1 (its region's last read: tile t - 1, phase 1)
-    //   phase 1: reads T2,     stages T0 + T1 of tile t + 2 (read in tile t's phase 0)
-    // so a third has ~2 phases to land; waits (R = KT - 1 - t):
-    //   phase 0 (T2(t)):         6 [R >= 1] pieces younger
-    //   phase 1 (T0, T1(t + 1)): 2 (1 + 2 [R >= 2]); R = 0: none
-    const int npro = min(5, 3 * KT);
-#pragma unroll
-    for (int q = 0; q < 5; ++q)
-      if (q < npro) stage(q % 3, q / 3);
-    if (KT >= 2)
-      vm_wait_nolgkm<6>();
-    else
-      vm_wait_nolgkm<2>();
-    if (wr == 1) bar();  // the skew
-    G256_RT(tl1);
-    auto ktile = [&](int kt, auto rem_c) {
-      constexpr int R = decltype(rem_c)::value;
-      const char* buf = bufof(kt);
-      read_a(buf, 0);
-      read_b(buf, 0);
-      if constexpr (R >= 1) stage(2, kt + 1);
-      vm_wait_nolgkm<R >= 1 ? 6 : 0>();
-      mma(0, 0);
-      bar();
-      read_b(buf, 1);
       if constexpr (R >= 2) {
         stage(0, kt + 2);
         stage(1, kt + 2);
       }
+      vm_wait_nolgkm<2 * ((R >= 1 ? 3 : 0) + (R >= 2 ? 2 : 0))>();
+      mma(0, 0);
+      bar();
+      // phase 1
+      read_b(buf, 1);
+      if constexpr (R == 0) ln_load();
+      if constexpr (R >= 2) stage(2, kt + 2);
       if constexpr (R >= 1)
-        vm_wait_nolgkm<2 * (1 + (R >= 2 ? 2 : 0))>();
+        vm_wait_nolgkm<2 * (1 + (R >= 2 ? 3 : 0))>();
       else
         bar();
       mma(0, 1);
@@ -431,6 +459,47 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     };
     for (int kt = 0; kt < KT - 2; ++kt) ktile(kt, std::integral_constant<int, 2>{});
     if (KT > 1) ktile(KT - 2, std::integral_constant<int, 1>{});
+    ktile(KT - 1, std::integral_constant<int, 0>{});
+    if (wr == 0) bar();  // the skew, closed
+  } else {
+    // 128 x 256 on two buffers (96 KiB: room for another kernel's 64 KiB workgroup on the CU).
+    //   phase 0: reads T0, T1, stages T0 + T1 of tile t + 1 (that buffer's T0 / T1: read by row 0 in
+    //            tile t - 1's phase 0, two phases earlier)
+    //   phase 1: reads T2,     stages T2 of tile t + 1 (read in tile t - 1's phase 1)
+    // so a region is restaged only after both wave rows' reads (the one-barrier skew; round 6, as
+    // above), and a third has ~2 phases to land; waits (R = KT - 1 - t):
+    //   phase 0 (T2(t)):         4 [R >= 1] pieces younger
+    //   phase 1 (T0, T1(t + 1)): 2; R = 0: none
+    const int npro = min(3, 3 * KT);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < npro) stage(q, 0);
+    vm_wait_nolgkm<2>();
+    if (wr == 1) bar();  // the skew
+    G256_RT(tl1);
+    auto ktile = [&](int kt, auto rem_c) {
+      constexpr int R = decltype(rem_c)::value;
+      const char* buf = bufof(kt);
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if constexpr (R >= 1) {
+        stage(0, kt + 1);
+        stage(1, kt + 1);
+      }
+      vm_wait_nolgkm<R >= 1 ? 4 : 0>();
+      mma(0, 0);
+      bar();
+      read_b(buf, 1);
+      if constexpr (R == 0) ln_load();
+      if constexpr (R >= 1) stage(2, kt + 1);
+      if constexpr (R >= 1)
+        vm_wait_nolgkm<2>();
+      else
+        bar();
+      mma(0, 1);
+      bar();
+    };
+    for (int kt = 0; kt < KT - 1; ++kt) ktile(kt, std::integral_constant<int, 1>{});
     ktile(KT - 1, std::integral_constant<int, 0>{});
     if (wr == 0) bar();  // the skew, closed
   }
@@ -519,12 +588,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
           float y = acc[a][b][v] + bv[b];
           if (g.res) {  // residual before the activation, as the general kernel (conv + BN + x -> ReLU)
             const size_t ri = (size_t)m * g.ldr + n;
-            y += g.res_f32 ? static_cast<const float*>(g.res)[ri]
-                           : static_cast<float>(static_cast<const _Float16*>(g.res)[ri]);
+            const _Float16* rh = static_cast<const _Float16*>(g.res);
+            y += RES == 3 ? static_cast<float>(rh[ri]) + static_cast<float>(rh[ri + g.plane])
+                 : g.res_f32 ? static_cast<const float*>(g.res)[ri]
+                             : static_cast<float>(rh[ri]);
           }
           y = finish(y);
           const size_t ci = (size_t)m * g.ldc + n;
-          if (g.out_f32)
+          if constexpr (RES == 3) {
+            _Float16* ch = static_cast<_Float16*>(g.C);
+            ch[ci] = static_cast<_Float16>(y);
+            ch[ci + g.plane] = static_cast<_Float16>(y - static_cast<float>(ch[ci]));
+          } else if (g.out_f32)
             static_cast<float*>(g.C)[ci] = y;
           else
             static_cast<_Float16*>(g.C)[ci] = static_cast<_Float16>(y);
@@ -573,16 +648,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     constexpr bool LNC = decltype(lnc_c)::value;
     constexpr bool LNO = decltype(lno_c)::value;
     constexpr int kRR = Geo::kRoundRows, kRounds = BM / kRR, kPasses = kRR / 16;  // rounds of the LDS-parked tile
-    [[maybe_unused]] float2 ln_st[kRounds];
     [[maybe_unused]] float c18[8];
-    if constexpr (LNC) {
-#pragma unroll
-      for (int h = 0; h < kRounds; ++h) {
-        float mean, rstd;
-        ln_row_stats(g.ln_in_stats, min(m0 + kRR * h + r0 + 16 * (cg & 7), g.M - 1), g.ln_in_chunks,
-                     g.ln_in_eps, mean, rstd);
-        ln_st[h] = float2{mean, rstd};
-      }
+    if constexpr (LNC) {  // the rows' {mean, rstd} (ln_st) from the partials the last k-tile loaded
+      static_assert(kRounds == kLnRounds, "epilogue rounds");
+      ln_combine();
       const floatx4 c0 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb);
       const floatx4 c1 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb + 4);
 #pragma unroll
@@ -596,16 +665,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       // residual rows: a ring of four rows per thread, the first four loaded before the park
       // (all eight at once would spill next to the accumulators the other wave row still holds)
       constexpr int PRE = 4;
-      half8 rvh[RES == 1 ? PRE : 1];
+      half8 rvh[RES == 1 || RES == 3 ? PRE : 1];
+      half8 rvl[RES == 3 ? PRE : 1];  // the lo plane's rows (RES = 3)
       floatx4 rvf[RES == 2 ? PRE : 1][2];
       auto res_row = [&](int pass) -> size_t {
         const int m = min(m0 + kRR * h + r0 + 16 * pass, g.M - 1);
         return (size_t)m * g.ldr + nb;
       };
-      if constexpr (RES == 1) {
+      if constexpr (RES == 1 || RES == 3) {
 #pragma unroll
-        for (int pass = 0; pass < PRE; ++pass)
+        for (int pass = 0; pass < PRE; ++pass) {
           rvh[pass] = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) + res_row(pass));
+          if constexpr (RES == 3)
+            rvl[pass] = *reinterpret_cast<const half8*>(static_cast<const _Float16*>(g.res) + res_row(pass) + g.plane);
+        }
       }
       if constexpr (RES == 2) {
 #pragma unroll
@@ -651,6 +724,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) r[e] = static_cast<float>(q[e]);
           }
+          if constexpr (RES == 3) {
+            const half8 qh = rvh[pass % PRE], ql = rvl[pass % PRE];
+            if (pass + PRE < kPasses) {
+              const _Float16* rp = static_cast<const _Float16*>(g.res) + res_row(pass + PRE);
+              rvh[pass % PRE] = *reinterpret_cast<const half8*>(rp);
+              rvl[pass % PRE] = *reinterpret_cast<const half8*>(rp + g.plane);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = static_cast<float>(qh[e]) + static_cast<float>(ql[e]);
+          }
           if constexpr (RES == 2) {
             const floatx4 q0 = rvf[pass % PRE][0], q1 = rvf[pass % PRE][1];
             if (pass + PRE < kPasses) {
@@ -668,7 +751,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] = e < 4 ? x0[e] : x1[e - 4];
           if constexpr (LNC) {  // LayerNorm of the A rows folded in: rstd (acc - mean c1)
-            const int src = (lane & 32) | pass;
+            const int src = (lane & 32) | (pass << 2);  // a lane of the four that combined this pass's row
             const float mean = __shfl(ln_st[h].x, src, 64), rstd = __shfl(ln_st[h].y, src, 64);
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] = rstd * (y[e] - mean * c18[e]);
@@ -697,17 +780,28 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
             if (m < g.M) {
               if ((cg & 7) == 0)
                 reinterpret_cast<float2*>(g.ln_out_stats)[(size_t)m * (g.N >> 6) + (nb >> 6)] = float2{mean, m2};
-              half8 hq;
+              if constexpr (RES != 3) {  // (two planes: the hi plane is the copy)
+                half8 hq;
 #pragma unroll
-              for (int e = 0; e < 8; ++e) hq[e] = static_cast<_Float16>(y[e]);
-              *reinterpret_cast<half8*>(g.c16 + (size_t)m * g.ld16 + nb) = hq;
+                for (int e = 0; e < 8; ++e) hq[e] = static_cast<_Float16>(y[e]);
+                *reinterpret_cast<half8*>(g.c16 + (size_t)m * g.ld16 + nb) = hq;
+              }
             }
           }
           if constexpr (GUARD) {
             if (m >= g.M) continue;
           }
           const size_t ci = (size_t)m * g.ldc + nb;
-          if constexpr (OUTF32) {
+          if constexpr (RES == 3) {
+            half8 oh, ol;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              oh[e] = static_cast<_Float16>(y[e]);
+              ol[e] = static_cast<_Float16>(y[e] - static_cast<float>(oh[e]));
+            }
+            *reinterpret_cast<half8*>(static_cast<_Float16*>(g.C) + ci) = oh;
+            *reinterpret_cast<half8*>(static_cast<_Float16*>(g.C) + ci + g.plane) = ol;
+          } else if constexpr (OUTF32) {
             *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci) = floatx4{y[0], y[1], y[2], y[3]};
             *reinterpret_cast<floatx4*>(static_cast<float*>(g.C) + ci + 4) = floatx4{y[4], y[5], y[6], y[7]};
           } else {
@@ -727,6 +821,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       epi(act_c, f32_c, std::true_type{}, lnc_c, lno_c);
   };
   auto by_act = [&](auto f32_c, auto lnc_c, auto lno_c) SPI_G256_EPI_INLINE {
+    if constexpr (RES >= 2) {
+      // fp32 / two-plane residual streams (the transformer out-proj / FFN2) carry no activation:
+      // the host routes such descs elsewhere, and their instances would only add register pressure
+      // (round 6: RES = 3 spilled 100 bytes per lane with ReLU / GELU instances, 0 without)
+      by_guard(std::integral_constant<int, (int)Act::None>{}, f32_c, lnc_c, lno_c);
+      return;
+    }
     if (act == Act::Gelu)
       by_guard(std::integral_constant<int, (int)Act::Gelu>{}, f32_c, lnc_c, lno_c);
     else if (act == Act::Relu)
@@ -745,12 +846,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       return;
     }
   }
-  if constexpr (RES == 2) {
+  if constexpr (RES == 2 || RES == 3) {  // (RES = 3: planes out, whatever OUTF32 says)
     if (g.ln_out) {
       by_act(T1{}, F{}, T1{});
       exit_stamp();
       return;
     }
+  }
+  if constexpr (RES == 3) {
+    by_act(F{}, F{}, F{});
+    exit_stamp();
+    return;
   }
   if (g.out_f32)
     by_act(T1{}, F{}, F{});
@@ -783,6 +889,8 @@ bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles, int bm) {
   if (min_tiles <= 0 || prec != Prec::F16 || d.conv || d.krep != 1 || d.a_split || d.out_split || d.pool_rows ||
       d.out_f16)
     return false;
+  if (d.res_planes != d.out_planes) return false;  // two planes: residual and output together (RES = 3)
+  if ((d.res_f32 || d.res_planes) && d.act != Act::None) return false;  // RES >= 2: no activation instances
   if (d.N % 256 || d.K % 64 || d.Kpad != d.K || d.lda % 8 || d.M < 1) return false;
   // no post-LN residual epilogue here (BERT's out-proj / FFN2 under the LayerNorm fold keep the
   // general kernel at every size; gemm256() rejects them)
@@ -790,7 +898,7 @@ bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles, int bm) {
   return (d.M + bm - 1) / bm * (d.N / 256) >= min_tiles;
 }
 
-void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm, int nbuf) {
+void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm, int nbuf, int n_fast) {
   if (d.N % 256 || d.K % 64 || d.Kpad != d.K) throw std::invalid_argument("gemm256: N % 256, K % 64, Kpad == K");
   if (bm != 256 && bm != 128) throw std::invalid_argument("gemm256: 256- or 128-row tiles");
   if (splits < 1 || splits > kMaxSplits || (splits > 1 && (!p.partial || !p.counters)))
@@ -828,8 +936,11 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, in
     throw std::invalid_argument("gemm256: the LayerNorm fold needs the vector epilogue");
   if (d.ln_in_chunks > 0 && (p.res || d.out_f32))
     throw std::invalid_argument("gemm256: the LayerNorm consumer fold is for fp16 outputs without a residual");
-  if (d.ln_out && (!p.res || !d.res_f32 || !d.out_f32))
-    throw std::invalid_argument("gemm256: the LayerNorm producer fold is for fp32 outputs over an fp32 residual");
+  const bool planes = d.res_planes || d.out_planes;
+  if (planes && (!d.res_planes || !d.out_planes || !p.res || d.out_f32 || d.plane % 8))
+    throw std::invalid_argument("gemm256: two planes for the residual and the output together");
+  if (d.ln_out && (!p.res || !((d.res_f32 && d.out_f32) || planes)))
+    throw std::invalid_argument("gemm256: the LayerNorm producer fold is for fp32 or two-plane outputs over the same residual");
   if (d.res_ln_chunks > 0) throw std::invalid_argument("gemm256: no residual LayerNorm (post-LN) epilogue");
   const int kt = d.K / 64;
   g.ktp = (kt + splits - 1) / splits;
@@ -837,29 +948,39 @@ void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, in
   if (g.splits != splits) throw std::invalid_argument("gemm256: splits must leave no empty slice");
   g.partial = p.partial;
   g.counters = p.counters;
-  const int res = !p.res ? 0 : d.res_f32 ? 2 : 1;
+  g.n_fast = n_fast ? 1 : 0;
+  g.plane = d.plane;
+  const int res = planes ? 3 : !p.res ? 0 : d.res_f32 ? 2 : 1;
+  if (res >= 2 && d.act != Act::None)
+    throw std::invalid_argument("gemm256: no activation over an fp32 / two-plane residual");
   const dim3 grid(g.tiles_m * g.tiles_n * g.splits), blk(512);
   if (bm == 256) {
     if (res == 0)
       SPI_LAUNCH((gemm256_kernel<0, 256, 2>), grid, blk, 0, s, g);
     else if (res == 1)
       SPI_LAUNCH((gemm256_kernel<1, 256, 2>), grid, blk, 0, s, g);
-    else
+    else if (res == 2)
       SPI_LAUNCH((gemm256_kernel<2, 256, 2>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<3, 256, 2>), grid, blk, 0, s, g);
   } else if (nbuf == 3) {
     if (res == 0)
       SPI_LAUNCH((gemm256_kernel<0, 128, 3>), grid, blk, 0, s, g);
     else if (res == 1)
       SPI_LAUNCH((gemm256_kernel<1, 128, 3>), grid, blk, 0, s, g);
-    else
+    else if (res == 2)
       SPI_LAUNCH((gemm256_kernel<2, 128, 3>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<3, 128, 3>), grid, blk, 0, s, g);
   } else {
     if (res == 0)
       SPI_LAUNCH((gemm256_kernel<0, 128, 2>), grid, blk, 0, s, g);
     else if (res == 1)
       SPI_LAUNCH((gemm256_kernel<1, 128, 2>), grid, blk, 0, s, g);
-    else
+    else if (res == 2)
       SPI_LAUNCH((gemm256_kernel<2, 128, 2>), grid, blk, 0, s, g);
+    else
+      SPI_LAUNCH((gemm256_kernel<3, 128, 2>), grid, blk, 0, s, g);
   }
 }
 

@@ -283,11 +283,13 @@ bool ln_fold_enabled(Prec prec, bool by_default) {
   const bool on = (e && *e) ? std::atoi(e) != 0 : by_default;
   return prec == Prec::F16 && on;
 }
-// BERT-base: fold +3.9 % four-stream (same process, round 4).  ViT-L: 5.93k with it against 6.30k
-// without (same process, profiles/r04/fixed/vit_fold_ab.txt): its long GEMMs gain less from the
-// removed launches than the producer epilogues (statistics + fp16 copy) cost them
+// BERT-base: fold +3.9 % four-stream (same process, round 4).  ViT-L: off in rounds 4-5 (5.93k
+// folded against 6.30k, profiles/r04/fixed/vit_fold_ab.txt: the producer epilogues' fp16 copy and
+// the consumers' statistics round trip + spills cost more than the 46 removed launches); on since
+// round 6 over the two-plane residual stream (no copy; statistics loaded under the last k-tile):
+// 6.68k folded against 6.59k (profiles/r06/vit_fold/)
 constexpr bool kBertLnFold = true;
-constexpr bool kVitLnFold = false;
+constexpr bool kVitLnFold = true;
 
 LnW pack_ln(const PMap& p, const std::string& name) {
   LnW l;
@@ -610,8 +612,8 @@ void Model::build_vit(const PMap& p) {
     ffn_ = L.ff1.n;
     tf_.push_back(L);
   }
-  // pre-LN: QKV of layer i >= 1 reads LN1_i(x) (layer 0's LN1 stays a launch: the stream
-  // comes from vit_assemble), FFN1 of layer i reads LN2_i(x)
+  // pre-LN: QKV of layer i >= 1 reads LN1_i(x) (layer 0's LN1 stays a launch, model body),
+  // FFN1 of layer i reads LN2_i(x)
   ln_fold_ = ln_fold_ && D_ % 128 == 0 && ffn_ % 128 == 0;
   if (ln_fold_) {
     for (int i = 0; i < layers_; ++i) {
@@ -846,12 +848,18 @@ void Model::run_conv_pair(const ConvW& c0, const void* x, int B, int H, int W, v
 }
 
 void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc, bool out_f32, Act act,
-                     const void* res, bool res_f32, int ldr, Workspace& ws, hipStream_t s, const LnSpec* ln) {
+                     const void* res, bool res_f32, int ldr, Workspace& ws, hipStream_t s, const LnSpec* ln,
+                     size_t planes) {
   GemmDesc d = linear_desc(L, M, lda, ldc);
   d.act = act;
   d.out_f32 = out_f32;
   d.res_f32 = res_f32;
   d.ldr = ldr;
+  if (planes) {  // C (and the residual, if any) in two fp16 planes `planes` elements apart
+    d.out_planes = true;
+    d.res_planes = res != nullptr;
+    d.plane = planes;
+  }
   d.wplane = L.wplane;
   LnPtrs lp;
   if (ln) {
@@ -879,8 +887,8 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   const size_t es = f16_ ? 2 : 4;
   const int nrep = !prof_ ? 1 : op_begin(s, "gemm_M" + std::to_string(M) + "_N" + std::to_string(L.n) + "_K" + std::to_string(L.k),
              2.0 * M * L.n * (double)L.k,
-             (double)M * L.k * es + (double)L.n * L.k * es + (double)M * L.n * (out_f32 ? 4 : es) +
-                 (res ? (double)M * L.n * (res_f32 ? 4 : es) : 0.0));
+             (double)M * L.k * es + (double)L.n * L.k * es + (double)M * L.n * (out_f32 || planes ? 4 : es) +
+                 (res ? (double)M * L.n * (res_f32 || planes ? 4 : es) : 0.0));
   GemmPtrs p;
   p.A = A;
   p.W = ptr<void>(L.w);
@@ -1229,40 +1237,58 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     float* x = static_cast<float*>(buf[2]);
     run_gemm(patch_proj_, buf[0], B * npatch_, patch_proj_.k, buf[1], D_, true, Act::None, nullptr, false, 0,
              w, s);
-    prof_op(s, "vit_assemble", (double)T * D_ * 4 * 3, [&] {
-      vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
-    });
+    if (!ln_fold_)
+      prof_op(s, "vit_assemble", (double)T * D_ * 4 * 3, [&] {
+        vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
+      });
     const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     if (ln_fold_) {
-      // Pre-LN with the LayerNorms folded (ln_fold.hpp): the GEMMs that update the residual
-      // stream x (in place) write its row statistics Sx and an fp16 copy (buf 3); the QKV
-      // (layer >= 1) and FFN1 GEMMs read that copy with LN1 / LN2 folded in.  Only layer 0's
-      // LN1 runs as a launch (x comes from vit_assemble).
+      // Pre-LN with the LayerNorms folded (ln_fold.hpp) over a two-plane residual stream (round 6,
+      // GemmDesc::res_planes): x lives in buf 2 as hi = fp16(x) and lo = fp16(x - hi), a plane of
+      // T x D apart -- the bytes of fp32, ~22-bit values.  vit_assemble_planes and the GEMMs that
+      // update x (out-proj, FFN2: residual and output both two-plane, in place) write the rows'
+      // chunk statistics Sx; the QKV GEMMs of layers >= 1 and every FFN1 GEMM read the hi plane as
+      // their fp16 A operand with LN1 / LN2 folded in.  No producer writes an fp16 copy (the hi
+      // plane is one).  Two LayerNorm launches are left: layer 0's LN1 (the stream's first rows
+      // come from the patch embedding, whose row means make the folded form lose ~20 % of the fp16
+      // margin: test_transformer_layernorm_fold, 8.5e-4 folded vs 7.0e-4 at this launch) and the
+      // class-token LayerNorm at the end.
       float* Sx = static_cast<float*>(buf[8]);
+      _Float16* xh = static_cast<_Float16*>(buf[2]);
+      const size_t plane = (size_t)T * D_;
+      prof_op(s, "vit_assemble", (double)T * D_ * 4 * 3, [&] {
+        vit_assemble_planes(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), xh, plane,
+                            nullptr, B, npatch_, D_, s);
+      });
       for (int i = 0; i < layers_; ++i) {
         const TfLayer& L = tf_[i];
         LnSpec q;
         if (i == 0) {
           prof_op(s, "layernorm", ln_bytes(T, false), [&] {
-            layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), nullptr, buf[3], D_, T, D_, eps_, f16_, s);
+            layernorm_planes(xh, plane, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), nullptr, buf[3], D_, T, D_,
+                             eps_, f16_, s);
           });
         } else {
           q.in_stats = Sx;
         }
-        run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
+        run_gemm(L.qkv, i == 0 ? buf[3] : xh, T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
         const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
                                                (double)T * 4 * D_ * 2);
         for (int r = 0; r < nrep; ++r) attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
         if (prof_) op_end(s);
         LnSpec o;
         o.out_stats = Sx;
-        o.c16 = buf[3];
-        run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s, &o);
+        run_gemm(L.out, buf[5], T, D_, xh, D_, false, Act::None, xh, false, D_, w, s, &o, plane);
         LnSpec f1;
         f1.in_stats = Sx;
-        run_gemm(L.ff1, buf[3], T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
-        run_gemm(L.ff2, buf[6], T, ffn_, x, D_, true, Act::None, x, true, D_, w, s, &o);
+        run_gemm(L.ff1, xh, T, D_, buf[6], ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
+        run_gemm(L.ff2, buf[6], T, ffn_, xh, D_, false, Act::None, xh, false, D_, w, s, &o, plane);
       }
+      prof_op(s, "layernorm_cls", ln_bytes(B, false), [&] {
+        layernorm_planes(xh, plane, S * D_, ptr<float>(final_ln_.g), ptr<float>(final_ln_.b), nullptr, buf[7], D_, B,
+                         D_, eps_, f16_, s);
+      });
+      return;
     } else {
     for (const TfLayer& L : tf_) {
       prof_op(s, "layernorm", ln_bytes(T, false), [&] {

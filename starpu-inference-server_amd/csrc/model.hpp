@@ -124,7 +124,7 @@ class Model {
   };
   void run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, int ldc,
                 bool out_f32, Act act, const void* res, bool res_f32, int ldr, Workspace& ws,
-                hipStream_t s, const LnSpec* ln = nullptr);
+                hipStream_t s, const LnSpec* ln = nullptr, size_t planes = 0);
   // QKV projection + attention of one transformer layer: the fused kernel (qkv_attn.hip) when
   // the shape allows it, else the QKV GEMM into qkv and the attention launch
   void run_qkv_attention(const LinearW& L, const void* x, const float* in_stats, void* qkv, void* ctx, int B,

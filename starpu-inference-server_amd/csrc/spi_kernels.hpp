@@ -93,6 +93,14 @@ struct GemmDesc {
   float res_ln_eps = 0.f;
   bool ln_out = false;
   int ld16 = 0;
+  // Two-plane fp16 residual stream (round 6, the transformer fold path): a row-major [rows][ld]
+  // tensor x kept as hi = fp16(x) at the pointer and lo = fp16(x - hi) `plane` elements further on
+  // -- ~22-bit values in the bytes of fp32, and the hi plane is already the fp16 operand the next
+  // folding GEMM reads, so a producer writes no separate fp16 copy (LnPtrs::c16 may be null).
+  // res_planes: the residual is such a pair; out_planes: C is written as one.
+  bool res_planes = false;
+  bool out_planes = false;
+  size_t plane = 0;
 };
 
 // Pointers of the LayerNorm fold (GemmDesc::ln_in_chunks / res_ln_chunks / ln_out).
@@ -103,7 +111,7 @@ struct LnPtrs {
   const float* res_g = nullptr;      // residual LayerNorm gain / bias
   const float* res_b = nullptr;
   float* out_stats = nullptr;        // output rows' chunk statistics
-  _Float16* c16 = nullptr;           // fp16 copy of the output
+  _Float16* c16 = nullptr;           // fp16 copy of the output (none with GemmDesc::out_planes)
 };
 
 struct GemmPtrs {
@@ -139,7 +147,8 @@ bool gemm256_eligible(const GemmDesc& d, Prec prec, int min_tiles, int bm = 256)
 // k-tiles (at most 4, at most max_split when > 0) to reach ~target workgroups (ViT-L's
 // N = 1024 GEMMs: 52 tiles -> FFN2 3 slices, out-proj none).
 int gemm256_splits(const GemmDesc& d, int target, int max_split, int bm = 256);
-void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm = 256, int nbuf = 2);
+void gemm256(const GemmDesc& d, const GemmPtrs& p, int splits, hipStream_t s, int bm = 256, int nbuf = 2,
+             int n_fast = 0);
 void gemm256_reload_env();  // no knobs left (kept for spi_debug_gemm_reload_env)
 
 // Fused QKV projection + attention for S <= 128 (qkv_attn.hip): one workgroup per (sequence,
@@ -203,6 +212,14 @@ void patchify(const float* x, void* y, int B, int C, int H, int W, int ps,
 // ViT: x[b, 0] = cls + pos[0]; x[b, 1+p] = patch[b, p] + pos[1+p]  (fp32).
 void vit_assemble(const float* patches, const float* cls, const float* pos,
                   float* x, int B, int P, int D, hipStream_t s);
+// The same into the two-plane residual stream (GemmDesc::res_planes: hi at xh, lo plane elements
+// on) plus, when stats is not null, each row's per-64-column chunk statistics [rows][D / 64][2]
+// (ln_fold.hpp).
+void vit_assemble_planes(const float* patches, const float* cls, const float* pos, _Float16* xh, size_t plane,
+                         float* stats, int B, int P, int D, hipStream_t s);
+// layernorm() over rows held in two fp16 planes (x = hi + lo), D <= 1024.
+void layernorm_planes(const _Float16* xh, size_t plane, int ldx, const float* g, const float* b, float* yf, void* yt,
+                      int ldy, int rows, int D, float eps, bool f16, hipStream_t s);
 // Gather rows: y[i] = x[i * stride_rows] (fp32 -> compute type) for CLS pooling.
 void gather_rows(const float* x, void* y, int rows, int stride_rows, int D,
                  bool f16, hipStream_t s);

@@ -96,3 +96,53 @@ def test_fast_erf_in_gemm_epilogues_meets_fp32_bar():
     assert e_erf < 5e-7 and e_gelu < 1e-6
     e16, g16 = mod.max_error(n=400_001, suffix="16")  # gemm256's lower-order form (fp16 operands)
     assert e16 < 3e-6 and g16 < 2e-6
+
+
+def test_bench_compact_line_fits_the_driver_tail(tmp_path):
+    """The printed line (bench.compact_line) carries the contract keys plus the metric's own
+    shapes -- ResNet-18 bs1 rate / p50, C3-C5, the CI workload, the CPU layouts -- and stays
+    under the 2000 bytes the driver's tail keeps; the full record goes to the detail file."""
+    import contextlib
+    import io
+    import json
+    long = "x" * 400  # long free-text fields must not reach the line
+    lay = {"value": 700.0, "p50_ms": 20.0, "workers": 16, "threads_per_worker": 1, "tasks": 100}
+    cfg_line = {"value": 24288.12, "unit": "sequences/s", "dtype": "fp16x3", "p50_task_latency_ms": 1.3532,
+                "roofline": {"frac": 0.13612, "selection": long}, "e2e": {"value": 22175.24, "p50_latency_ms": 5.7508}}
+    full = {
+        "metric": bench.BASELINE_METRIC, "value": 116656.42, "unit": "inferences/s", "n_gpus": 8, "steps": 20,
+        "warmup": 5, "ms_per_step": 2.1945, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp16m", "data": long,
+        "config": {"workload": bench.WORKLOADS["resnet18"], "batch_per_task": 8, "workers_per_gpu": 4,
+                   "tasks_per_step": 8, "parallelism": "replicas x8 (request sharding, no collective)",
+                   "precision_mode": long},
+        "roofline": {"bound": "mfma", "achieved": 149.146, "peak": 2500.0, "unit": "TFLOP/s", "frac": 0.05966,
+                     "traffic": 14356821, "kernel": "conv3x3_c512_k512_s1_M392", "avg_launch_ms": 0.0124,
+                     "frac_rocprof": 0.05709, "mfma_busy_pct": 3.86, "selection": long, "measured": long},
+        "cpu_baseline": {"value": 784.734, "unit": "inferences/s", "cores": 16, "kind": "port", "sample": long,
+                         "sample_short": "y" * 180, "host": {"nproc": 256, "numa_nodes": 2},
+                         "layouts_summary": {f"bs{b}_{t}": [12345.678, 123.456, 16, 16] for b in (8, 1)
+                                             for t in ("i", "ii", "iii")}},
+        "e2e": {"value": 80824.12, "p50_latency_ms": 3.0912, "p99_latency_ms": 3.2145, "breakdown_ms": long},
+        "p50_task_latency_ms": 0.273,
+        "extras": {"resnet18_bs1_tasks": {"value": 20876.02, "p50_task_latency_ms": 0.1946,
+                                          "p50_serial_e2e_latency_ms": 0.2147},
+                   "c3_bert_base_seq128_bs8_fp16": cfg_line, "c4_resnet152_bs32_fp16x3": cfg_line,
+                   "c5_vit_l_16_bs16_fp16": cfg_line,
+                   "ci_perf_resnet152_schedule": {"value": 443.98, "p50_latency_ms": 9.5478, "config": long,
+                                                  "mi355x_tuned": {"value": 443.98, "p50_latency_ms": 1.7066}}},
+    }
+    buf = io.StringIO()
+    detail = tmp_path / "detail.json"
+    with contextlib.redirect_stdout(buf):
+        bench.emit(full, str(detail))
+    text = buf.getvalue().strip()
+    assert "\n" not in text and len(text) < 2000, len(text)
+    line = json.loads(text)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line
+    assert line["config"]["workload"] == bench.WORKLOADS["resnet18"]
+    assert line["resnet18_bs1"]["p50_task_ms"] == 0.1946 and line["c3_bert"]["value"] == 24288.12
+    assert line["ci_perf"]["tuned_p50_ms"] == 1.7066 and line["cpu_baseline"]["nproc"] == 256
+    assert json.loads(detail.read_text())["data"] == long
