@@ -855,9 +855,9 @@ void Model::run_gemm(const LinearW& L, const void* A, int M, int lda, void* C, i
   d.out_f32 = out_f32;
   d.res_f32 = res_f32;
   d.ldr = ldr;
-  if (planes) {  // C (and the residual, if any) in two fp16 planes `planes` elements apart
+  if (planes) {  // C (and an fp16-typed residual) in two fp16 planes `planes` elements apart
     d.out_planes = true;
-    d.res_planes = res != nullptr;
+    d.res_planes = res != nullptr && !res_f32;
     d.plane = planes;
   }
   d.wplane = L.wplane;
@@ -1181,19 +1181,25 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
     float* a = static_cast<float*>(w.bufs[4]);
     void* ff = w.bufs[5];
     if (ln_fold_) {
-      // Post-LN with the LayerNorms folded (ln_fold.hpp): hf holds the embedding output, then
-      // each layer's pre-LN2 rows b; a the pre-LN1 rows; ht the fp16 copy the next GEMM reads;
-      // S1 / S2 their row statistics.  Layer i:
-      //   qkv  = LN2_{i-1}(b) Wqkv  (folded; layer 0 reads the embedding output)
-      //   a    = ctx Wo + LN2_{i-1}(b)    -> S1, ht
+      // Post-LN with the LayerNorms folded (ln_fold.hpp) over two-plane fp16 rows (round 6,
+      // GemmDesc::res_planes: hi = fp16(x), lo = fp16(x - hi), a plane of T x D apart, the bytes of
+      // fp32): buf 0 holds the embedding output (fp32, the prologue's), then each layer's pre-LN2
+      // rows b as planes; buf 4 the pre-LN1 rows a as planes; S1 / S2 their row statistics.  The hi
+      // planes are the folding GEMMs' fp16 A operands, so no producer writes an fp16 copy.
+      // Layer i:
+      //   qkv  = LN2_{i-1}(b) Wqkv  (folded; layer 0 reads the embedding's fp16 output ht)
+      //   a    = ctx Wo + LN2_{i-1}(b)    -> S1   (layer 0: + the fp32 embedding output)
       //   ff   = GELU(LN1_i(a) W1)  (folded)
-      //   b    = ff W2 + LN1_i(a)         -> S2, ht
+      //   b    = ff W2 + LN1_i(a)         -> S2
       // and the epilogue runs the one LayerNorm left, LN2 of the last layer.
       float* S1 = static_cast<float*>(w.bufs[6]);
       float* S2 = static_cast<float*>(w.bufs[7]);
+      _Float16* bh = static_cast<_Float16*>(w.bufs[0]);
+      _Float16* ah = static_cast<_Float16*>(w.bufs[4]);
+      const size_t plane = (size_t)T * D_;
       for (int i = 0; i < layers_; ++i) {
         const TfLayer& L = tf_[i];
-        run_qkv_attention(L.qkv, ht, i > 0 ? S2 : nullptr, qkv, ctx, B, S, w, s);
+        run_qkv_attention(L.qkv, i > 0 ? bh : ht, i > 0 ? S2 : nullptr, qkv, ctx, B, S, w, s);
         LnSpec o;
         if (i > 0) {
           o.res_stats = S2;
@@ -1201,18 +1207,17 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
           o.res_b = ptr<float>(tf_[i - 1].ln2.b);
         }
         o.out_stats = S1;
-        o.c16 = ht;
-        run_gemm(L.out, ctx, T, D_, a, D_, true, Act::None, hf, true, D_, w, s, &o);
+        run_gemm(L.out, ctx, T, D_, ah, D_, false, Act::None, i > 0 ? static_cast<void*>(bh) : hf, i == 0, D_, w, s,
+                 &o, plane);
         LnSpec f1;
         f1.in_stats = S1;
-        run_gemm(L.ff1, ht, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
+        run_gemm(L.ff1, ah, T, D_, ff, ffn_, false, Act::Gelu, nullptr, false, 0, w, s, &f1);
         LnSpec f2;
         f2.res_stats = S1;
         f2.res_g = ptr<float>(L.ln1.g);
         f2.res_b = ptr<float>(L.ln1.b);
         f2.out_stats = S2;
-        f2.c16 = ht;
-        run_gemm(L.ff2, ff, T, ffn_, hf, D_, true, Act::None, a, true, D_, w, s, &f2);
+        run_gemm(L.ff2, ff, T, ffn_, bh, D_, false, Act::None, ah, false, D_, w, s, &f2, plane);
       }
       return;
     }
@@ -1327,9 +1332,13 @@ void Model::epilogue(Workspace& w, int B, int S, void* const* out, hipStream_t s
     const TfLayer& L = tf_.back();
     const int T = B * S;
     prof_op(s, "layernorm_out", (double)T * D_ * 8, [&] {
-      // the last layer's pre-LN2 rows: hf under the LayerNorm fold, else a
-      layernorm(static_cast<float*>(w.bufs[ln_fold_ ? 0 : 4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
-                static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
+      // the last layer's pre-LN2 rows: the two-plane b (buf 0) under the LayerNorm fold, else a
+      if (ln_fold_)
+        layernorm_planes(static_cast<const _Float16*>(w.bufs[0]), (size_t)T * D_, D_, ptr<float>(L.ln2.g),
+                         ptr<float>(L.ln2.b), static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
+      else
+        layernorm(static_cast<float*>(w.bufs[4]), D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b),
+                  static_cast<float*>(out[0]), nullptr, D_, T, D_, eps_, f16_, s);
     });
   } else if (family_ == SPI_FAMILY_VIT) {
     run_gemm(head_, w.bufs[7], B, D_, out[0], classes_, true, Act::None, nullptr, false, 0, w, s);

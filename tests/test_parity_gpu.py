@@ -190,19 +190,16 @@ def test_vit_small_seq197(spi, zoo, gpu, prec):
 def test_transformer_layernorm_fold(spi, zoo, gpu, family, prec, monkeypatch):
     """The LayerNorm fold (ln_fold.hpp, DESIGN.md 3.6: statistics from the producing GEMM's
     epilogue, gain folded into the consuming GEMM's weights, post-LN residuals recomputed
-    element-wise) against the separate LayerNorm launches (SPI_LN_FOLD=0) and the oracle; the
-    folded forward runs at most two LayerNorm launches.  The weights here are drawn wider than
-    HF's init (std 0.05, larger activations and row means: the fold's cancellation case).
-    fp16m (hi + lo weights on every GEMM) holds both paths under the 1e-3 bar.  Plain fp16 sits
-    at the bar on this model: the CPU emulation of the fp16 path (tools/prec_emulate_bert.py)
-    puts the unfused path at 1.00e-3 and the folded one at 1.04e-3, spread over every rounding
-    site (weights 0.35e-3 of it, no other site more than 0.1e-3), so its bar is
-    that the fold is no less accurate than the launches it replaces (within 10 %) and within
-    1.5e-3 -- the 1e-3 bars of the BASELINE configs are test_bert_base_seq128_bs8 / the full-size
-    tests."""
+    element-wise, the two-plane residual rows of round 6) against the separate LayerNorm launches
+    (SPI_LN_FOLD=0) and the oracle, every path at the 1e-3 bar; the folded forward runs at most two
+    LayerNorm launches.  fp16m's BERT is drawn wider than HF's init (std 0.05: larger activations
+    and row means), where plain fp16 arithmetic itself -- folded or not -- sits at the bar (CPU
+    emulation, tools/prec_emulate_bert.py: unfused 1.00e-3, folded 1.04e-3, spread over every
+    rounding site); plain fp16 runs HF's init here, and its fold is stressed by the
+    outlier-dimension and large-row-mean fixtures of test_bert_layernorm_fold_outliers."""
     rng = np.random.default_rng(13)
     if family == "bert":
-        m = zoo.bert(layers=3, init_std=0.05)
+        m = zoo.bert(layers=3, init_std=0.05 if prec == "fp16m" else 0.02)
         ids, mask = bert_inputs(rng, 3, 80, pad_from=50)
         inputs, kw = [ids, mask], dict(max_batch=3, seq_len=128)
     else:
@@ -222,10 +219,51 @@ def test_transformer_layernorm_fold(spi, zoo, gpu, family, prec, monkeypatch):
     e_f, e_p = normalized_max_error(folded, ref), normalized_max_error(plain, ref)
     print(f"{family} {prec} LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e}), LN launches {n_ln}")
     assert n_ln <= 2
-    if prec == "fp16m":
-        assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3, (e_f, e_p, d)
-    else:
-        assert e_f < 1.5e-3 and e_f <= 1.1 * e_p, (e_f, e_p, d)
+    assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3, (e_f, e_p, d)
+
+
+def bert_with_outliers(zoo, kind, layers=3):
+    """BERT at HF's init (std 0.02) with the LayerNorm structure that makes trained checkpoints hard
+    for fp16: "dims" -- three outlier dimensions (gain 8, bias +-3 in every
+    LayerNorm: the residual stream carries a few features an order of magnitude above the rest,
+    as in pretrained BERT); "offset" -- every LayerNorm bias shifted by +2 (rows whose mean is twice
+    their spread: the folded form's cancellation case, rstd (x W' - mean c1))."""
+    m = zoo.bert(layers=layers)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.LayerNorm):
+                if kind == "dims":
+                    for d, sgn in ((17, 1.0), (308, -1.0), (555, 1.0)):
+                        mod.weight[d] = 8.0
+                        mod.bias[d] = 3.0 * sgn
+                else:
+                    mod.bias.add_(2.0)
+    return m
+
+
+@pytest.mark.parametrize("kind", ["dims", "offset"])
+def test_bert_layernorm_fold_outliers(spi, zoo, gpu, kind, monkeypatch):
+    """The plain-fp16 LayerNorm fold (C3's serving path) on outlier-dimension and large-row-mean
+    BERT (bert_with_outliers) against the separate LayerNorm launches and the oracle, at the
+    north_star 1e-3 bar."""
+    rng = np.random.default_rng(17)
+    m = bert_with_outliers(zoo, kind)
+    ids, mask = bert_inputs(rng, 3, 80, pad_from=50)
+    ref = cpu_inference(m, [ids, mask])[0]
+    kw = dict(max_batch=3, seq_len=128)
+    monkeypatch.setenv("SPI_LN_FOLD", "1")
+    folded = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), [ids, mask], ref.shape, graphs=True)
+    monkeypatch.setenv("SPI_LN_FOLD", "0")
+    plain = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", **kw), [ids, mask], ref.shape)
+    d = normalized_max_error(folded, plain)
+    e_f, e_p = normalized_max_error(folded, ref), normalized_max_error(plain, ref)
+    # the outlier features set max|ref|: hold the ordinary features to the bar on their own scale too
+    keep = np.ones(ref.shape[-1], bool)
+    keep[[17, 308, 555]] = False
+    e_k = normalized_max_error(folded[..., keep], ref[..., keep])
+    print(f"bert outliers {kind} fp16 LN fold: vs unfused {d:.3e}, vs oracle {e_f:.3e} (unfused {e_p:.3e}), "
+          f"ordinary features {e_k:.3e}")
+    assert e_f < 1e-3 and e_p < 1e-3 and d < 1e-3 and e_k < 1e-3, (e_f, e_p, d, e_k)
 
 
 @pytest.mark.parametrize("family", ["vit", "bert"])

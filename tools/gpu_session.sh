@@ -8,6 +8,8 @@
 #   bench                   the default bench line (bench.py), summary printed
 #   loop=MODEL:B:PREC       the timed loop only (bench.py --loop-only)
 #   sweep=MODEL:B:PREC:POL;POL;...   tools/policy_sweep.py, POL = NAME=KEY=VAL[&KEY=VAL] (3 rounds)
+#   ab=MODEL:B:PREC:LIB,LIB,...  timed loops of several library builds (tools/build_variant.sh;
+#                           "base" = the in-tree library), processes interleaved, 3 rounds
 #   pmc=MODEL:B:PREC        PMC traffic + MFMA-busy per op (tools/pmc_traffic.sh)
 #   trace=MODEL:B:PREC      rocprofv3 trace of the timed loop regrouped per op (tools/trace_round.sh)
 #   roofline                rocprofv3 roofline summaries of every config (tools/round_profile.sh, SKIP_TRACE=1)
@@ -51,6 +53,17 @@ for step in "$@"; do
       for x in "${pl[@]}"; do args+=(--policy "$x"); done
       timeout -k 10 600 python -u tools/policy_sweep.py --model "$m" --batch "$b" --precision "$p" "${args[@]}" > "$log" 2>&1 || fail "$step" "$log"
       cat "$log" ;;
+    ab)
+      IFS=: read -r m b p libs <<< "$val"
+      IFS=',' read -ra ll <<< "$libs"
+      for rep in 1 2 3; do
+        for lib in "${ll[@]}"; do
+          l=""; [ "$lib" != base ] && l=$lib
+          SPI_HIP_LIB=$l timeout -k 10 300 python -u bench.py --loop-only --model "$m" --batch "$b" --precision "$p" \
+            --steps 20 --warmup 5 > "$log.tmp" 2>&1 || fail "$step" "$log.tmp"
+          echo "$(basename "$lib") $rep $(tail -1 "$log.tmp")" | tee -a "$log"
+        done
+      done ;;
     pmc)
       IFS=: read -r m b p <<< "$val"
       timeout -k 10 900 bash tools/pmc_traffic.sh "$O/pmc_${m}_bs${b}_${p}" --model "$m" --batch "$b" --precision "$p" --iters 12 > "$log" 2>&1 || fail "$step" "$log"
