@@ -1719,8 +1719,12 @@ struct Knobs {
   int win = 1;
   int g256_min = 128;      // SPI_GEMM_256_MIN="T256[,T128]": dense F16 GEMMs with >= T256 tiles of 256^2 -> gemm256 (0 = off)
   // ... else with >= T128 tiles of 128 x 256 -> gemm256's 128-row tile (round 5; 0 = off)
-  int g128_min = 0;  // off by default: under the four worker streams BERT -7 %, ViT-L -1 %
-  int g128_nbuf = 3;  // third field: k-tile buffers of the 128-row tile (2: 96 KiB, 3: 144 KiB)
+  // round 6: 64 tiles, two buffers -- BERT-base's FFN1 (96 tiles of 128 x 256, K = 768) four-stream
+  // +1.5 % (24.25k -> 24.60k, profiles/r06/sweeps/); the long-K rule below keeps ViT-L's N = 1024
+  // GEMMs on 256^2 tiles (128 x 256 there: -3 % with three buffers, -7 % with two).  Rounds 3-5
+  // had it off (BERT -7 % with the three-buffer schedule, which also raced)
+  int g128_min = 64;
+  int g128_nbuf = 2;  // third field: k-tile buffers of the 128-row tile (2: 96 KiB, 3: 144 KiB)
   // SPI_GEMM_256_LONGK="tiles,K": also with >= `tiles` tiles when K >= `K` (round 3: 48,1024 -- ViT-L FFN2 /
   // out-proj, 52 tiles: one 256^2 workgroup per CU-time unit does ~1.7x the work of the 128x128 kernel, so
   // under four streams ViT-L goes 6.07k -> 6.70k inf/s though the launch alone is slower; BERT's K = 768
@@ -1818,15 +1822,15 @@ Knobs& knobs() {
 }
 
 // gemm256 routing by desc (gemm() also needs 16-byte aligned A / W): the tile height it runs
-// at, 0 = the general kernel.  256^2 tiles for grids of >= T256 of them; else 128 x 256 tiles
-// for grids of >= T128 of those (BERT-base's QKV / FFN1 at bs8: 72 / 96, ViT-L's N = 1024
-// GEMMs at bs16: 100 instead of 52 256^2 tiles); else 256^2 on the long-K rule.
+// at, 0 = the general kernel.  256^2 tiles for grids of >= T256 of them, or of >= the long-K
+// rule's tiles when K is long (ViT-L's N = 1024 GEMMs at bs16: 52 tiles); else 128 x 256 tiles
+// for grids of >= T128 of those (BERT-base's FFN1 at bs8: 96).
 int route_bm(const GemmDesc& d, Prec prec) {
   const Knobs& k = knobs();
   if (prec != Prec::F16) return 0;
   if (gemm256_eligible(d, prec, k.g256_min)) return 256;
-  if (gemm256_eligible(d, prec, k.g128_min, 128)) return 128;
   if (k.g256_longk_tiles > 0 && d.K >= k.g256_longk_k && gemm256_eligible(d, prec, k.g256_longk_tiles)) return 256;
+  if (gemm256_eligible(d, prec, k.g128_min, 128)) return 128;
   return 0;
 }
 bool routes_256(const GemmDesc& d, Prec prec) { return route_bm(d, prec) != 0; }
