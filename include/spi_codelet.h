@@ -239,11 +239,13 @@ enum spi_family {
  * hi + lo fp16 halves, hi*hi + hi*lo + lo*hi per fragment (fp32-grade
  * results at the fp16 MFMA rate).
  * SPI_PREC_F16M, ResNet: fp16 activations and fp16 MFMA operands everywhere except
- * the precision-critical layers -- the stem (fp32 image x split weights), the
- * downsample 1x1 convs (fp16 activations x hi + lo weights, fp32 out) and the FC
- * (fp32 pooled features x split weights).  BERT / ViT: the F16 path with hi + lo
- * weights on every GEMM (two fp16 MFMAs per fragment pair: the weights' rounding
- * is the largest of the fp16 path's error sites, tools/prec_emulate_bert.py). */
+ * the precision-critical layers -- the stem (the image rounded to fp16 x hi + lo
+ * weights, fp16 out) and the downsample 1x1 convs (fp16 activations x hi + lo weights,
+ * fp16 out); the FC runs on plain fp16 weights (round 5: CPU emulation worst case
+ * 0.74e-3 over 8 input seeds against the 1e-3 bar, GPU 0.60-0.69e-3).  BERT / ViT: the
+ * F16 path with hi + lo weights on every GEMM (two fp16 MFMAs per fragment pair: the
+ * weights' rounding is the largest of the fp16 path's error sites,
+ * tools/prec_emulate_bert.py). */
 enum spi_precision { SPI_PREC_F32 = 0, SPI_PREC_F16 = 1, SPI_PREC_F16X3 = 2, SPI_PREC_F16M = 3 };
 
 typedef struct spi_named_tensor {

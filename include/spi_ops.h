@@ -66,8 +66,9 @@ int spi_op_avgpool_fc(int32_t precision, const void* x, int32_t B, int32_t HW, i
 
 /* Fused ResNet stem: x NCHW fp32 [B][3][H][W] -> 7x7/s2/p3 conv (64 channels,
  * BN folded into w / bias) + ReLU -> 3x3/s2/p1 max pool -> y NHWC [B][PH][PW][64].
- * precision 1: fp16 operands, fp16 y; 2: hi + lo fp16 operands (fp32-grade), fp16 y
- * (the fp16m stem); 3: as 2 with y in the split layout.  W_packed: spi_op_stem_pool_bytes()
+ * precision 1: fp16 image and weights, fp16 y; 2: the fp16m stem -- fp16 image x hi + lo fp16
+ * weights, fp16 y; 3: hi + lo image x hi + lo weights (fp32-grade), y in the split layout (the
+ * fp16x3 stem); 4: as 3 with fp16 y.  W_packed: spi_op_stem_pool_bytes()
  * of device memory filled from spi_op_stem_pool_pack(w_host fp32 [64][3][7][7]).
  * rows_per_block: 0 = default (2 pooled rows per 8-wave workgroup for maps wider than 64,
  * else 1 per 4 waves), 1 or 2 = that many per 4-wave workgroup.  W <= 224. */

@@ -75,7 +75,9 @@ typedef struct spi_batching_config {
   /* This build's MI355X tuning (not in the reference): a worker with no task in flight
    * dispatches what the queue holds at once (up to the strategy's target) instead of
    * waiting up to coalesce_timeout_us for more jobs; batches still form from the jobs
-   * that queue while every worker is busy.  0 = the reference's collector. */
+   * that queue while every worker is busy.  0 = the reference's collector.  Applies to
+   * SPI_BATCHING_ADAPTIVE only: the FIXED kind ignores it and keeps coalesce_max_jobs /
+   * coalesce_delay_us. */
   int32_t idle_dispatch;
   int32_t _pad1;
 } spi_batching_config;

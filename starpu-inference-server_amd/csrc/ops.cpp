@@ -189,12 +189,14 @@ int spi_op_stem_pool_pack(const float* w, void* dst) {
 
 int spi_op_stem_pool(int32_t precision, const float* x, int32_t B, int32_t H, int32_t W, const void* Wp,
                      const float* bias, void* y, int32_t rows_per_block, void* stream) {
-  if (precision < 1 || precision > 3 || !x || !Wp || !bias || !y || B <= 0 || H <= 0 || W <= 0 ||
+  if (precision < 1 || precision > 4 || !x || !Wp || !bias || !y || B <= 0 || H <= 0 || W <= 0 ||
       rows_per_block < 0 || rows_per_block > 2)
     return fail("invalid stem_pool arguments");
   if ((W + 6 - 7) / 2 + 1 > spi::kStemPoolMaxOW) return fail("stem_pool: image wider than 224");
-  spi::stem_pool(x, Wp, bias, y, B, H, W, precision >= 2 ? 2 : 0, precision == 3, rows_per_block,
-                 static_cast<hipStream_t>(stream));
+  // stem_pool's lo: 0 fp16 weights, 1 hi + lo weights on the fp16 image (the model's fp16m stem),
+  // 2 hi + lo weights on the split image (fp32-grade; fp16x3 and the split output)
+  const int lo = precision == 1 ? 0 : precision == 2 ? 1 : 2;
+  spi::stem_pool(x, Wp, bias, y, B, H, W, lo, precision == 3, rows_per_block, static_cast<hipStream_t>(stream));
   return check_launch();
 }
 

@@ -448,8 +448,10 @@ bool spi_runtime::compose(Worker* w, std::unique_lock<std::mutex>& lk, std::vect
   // idle_dispatch (this build's tuning): an idle worker does not wait at all -- on the
   // reference's CI workload the 10 ms coalescer held requests while the GPU sat idle
   // (p50 queue 8.25 of 11.2 ms); under load the queue fills while every worker is busy
-  // and the next free worker takes a batch of it anyway.
-  if (timeout_us > 0 && w->inflight.empty() && !bc.idle_dispatch) {
+  // and the next free worker takes a batch of it anyway.  The adaptive strategy's option only:
+  // the FIXED kind keeps its coalesce_max_jobs / coalesce_delay_us merging.
+  const bool idle_now = bc.idle_dispatch && bc.kind == SPI_BATCHING_ADAPTIVE;
+  if (timeout_us > 0 && w->inflight.empty() && !idle_now) {
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
     while (!stop && (int)jobs.size() < max_jobs && total < target) {
       if (cv_job.wait_until(lk, deadline) == std::cv_status::timeout) {

@@ -134,7 +134,9 @@ def avgpool_fc(prec, x, W_packed, N_, bias=None, act=None, ws=None, stream=None)
     return out
 
 
-STEM_PREC = {"fp16": 1, "fp16m": 2, "fp16x3s": 3}  # fp16 operands / hi+lo operands, fp16 out / ... split out
+# fp16 operands / fp16 image x hi+lo weights (the model's fp16m stem) / hi+lo image x hi+lo weights, split out
+# (fp16x3s) or fp16 out (fp16x3)
+STEM_PREC = {"fp16": 1, "fp16m": 2, "fp16x3s": 3, "fp16x3": 4}
 
 
 def stem_pool(prec, x_nchw, w_folded, bias, rows_per_block=0, stream=None):

@@ -338,19 +338,23 @@ def stem_pool_ref(x, w, b):
     return F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1).permute(0, 2, 3, 1)
 
 
-@pytest.mark.parametrize("prec", ["fp16", "fp16m", "fp16x3s"])
+@pytest.mark.parametrize("prec", ["fp16", "fp16m", "fp16x3s", "fp16x3"])
 @pytest.mark.parametrize("B,H,W,rows", [(8, 224, 224, 0), (8, 224, 224, 2), (3, 64, 64, 0), (1, 65, 47, 0),
                                         (2, 33, 17, 2), (1, 9, 9, 0), (2, 223, 224, 1)])
 def test_stem_pool_fused(ops, prec, B, H, W, rows):
     """Fused stem (NCHW fp32 image -> 7x7/s2 conv + bias + ReLU -> 3x3/s2 max pool, one launch)
     vs F.conv2d / relu / max_pool2d: odd sizes exercise the partial column blocks, the pool's
-    edge windows and a last workgroup with fewer pooled rows than rows_per_block."""
+    edge windows and a last workgroup with fewer pooled rows than rows_per_block.  fp16m is the
+    stem the fp16m model runs (fp16 image x hi + lo weights; ADVICE r05: the op test had covered
+    the split-image kernel only)."""
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + W + rows)
     x = torch.rand(B, 3, H, W, generator=g)
     w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
     b = torch.randn(64, generator=g) * 0.1
     if prec == "fp16":
         ref = stem_pool_ref(x.half().float(), w.half().float(), b)
+    elif prec == "fp16m":  # the image rounded to fp16, the weights at ~22 bits
+        ref = stem_pool_ref(x.half().double(), w.double(), b.double()).float()
     else:
         ref = stem_pool_ref(x.double(), w.double(), b.double()).float()
     out = ops.stem_pool(prec, x.cuda(), w, b.cuda(), rows_per_block=rows)

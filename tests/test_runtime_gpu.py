@@ -303,6 +303,28 @@ def test_runtime_idle_dispatch_skips_the_coalescer(spi, zoo, rtmod):
     assert p50[True] < 5.0 < p50[False]
 
 
+def test_runtime_idle_dispatch_leaves_fixed_batching_alone(spi, zoo, rtmod):
+    """idle_dispatch is the adaptive strategy's option (include/spi_runtime.h): under the FIXED
+    kind the worker still merges up to coalesce_max_jobs jobs, waiting up to coalesce_delay_us
+    for them.  A burst of 8 requests every 20 ms against a 10 ms delay: the tasks carry the
+    burst whole (mean task batch well above 1) with or without the flag."""
+    m = zoo.resnet18(image=64)
+    rep = spi.ModelReplica(m, 0, "fp16", max_batch=8, image_size=64, graphs=True)
+    x = np.random.default_rng(15).random((1, 3, 64, 64), dtype=np.float32)
+    batch = {}
+    for idle in (False, True):
+        b = rtmod.batching_config("fixed", idle_dispatch=idle)
+        rt = rtmod.Runtime([rep], [((3, 64, 64), np.float32)], [(1000, np.float32)], max_batch=8,
+                           workers_per_device=1, max_queue=64, coalesce_max_jobs=8, coalesce_delay_us=10_000,
+                           batching=b)
+        r = rt.loadgen([x], schedule=[(0, 8), (20_000, 1), (0, 7), (20_000, 1), (0, 7)])
+        assert r["completed"] == 24 and r["failed"] == 0
+        batch[idle] = r["mean_task_batch"]
+        rt.close()
+    print(f"fixed kind: mean task batch {batch[False]:.2f} without idle_dispatch, {batch[True]:.2f} with")
+    assert batch[False] > 3 and batch[True] > 3
+
+
 def test_runtime_loadgen_closed_and_open_loop(spi, zoo, rtmod):
     """The C++ client loop: closed loop with k requests outstanding, and the open-loop
     (delta_us, repeat) schedule of ci/perf/ci_perf_resnet.csv with a bounded queue."""

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Roofline evidence of a round (ROUND=r05 by default) for every BASELINE GPU config (run through gpurun from the repo root):
+# Roofline evidence of a round (ROUND=r06 by default) for every BASELINE GPU config (run through gpurun from the repo root):
 #   1. tools/trace_round.sh: rocprofv3 kernel trace of each config's graph-replayed timed loop,
 #      regrouped per op (gpurun_out/trace/trace_<cfg>_ops.csv + kernel stats);
 #   2. the trace CSVs copied into profiles/$ROUND/ of this (scratch) tree, so bench.py's roofline
@@ -7,9 +7,9 @@
 #   3. per config, rocprofv3 --kernel-trace --stats of `bench.py --roofline-only` for the top op
 #      of its trace (the back-to-back launches the bench line times) -> gpurun_out/rl_$ROUND/
 #      roofline_rocprof.json (tools/rocprof_roofline.py) + roofline_<cfg>_kernel_stats.csv.
-# usage: bash tools/round4_profile.sh
+# usage: ROUND=r06 bash tools/round_profile.sh
 set -euo pipefail
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 export TMPDIR=/tmp
 cfgs=(resnet18:8:fp16m bert_base:8:fp16 resnet152:32:fp16x3 vit_l_16:16:fp16)
 if [ "${SKIP_TRACE:-0}" != 1 ]; then  # SKIP_TRACE=1: the committed profiles/$ROUND traces pick the ops
