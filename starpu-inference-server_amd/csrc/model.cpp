@@ -375,7 +375,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     os << "] img" << image_ << " classes" << classes_;
   } else if (family_ == SPI_FAMILY_BERT) {
     mixed_ = cfg.precision == SPI_PREC_F16M;  // hi + lo weights on every encoder GEMM
-    if (const char* e = std::getenv("SPI_QKV_ATTN"); e && *e) qkv_fused_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SPI_QKV_ATTN"); e && *e) qkv_fused_ = std::atoi(e);
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-12f;
     ln_fold_ = ln_fold_enabled(prec_, kBertLnFold);
     heads_ = cfg.num_heads;
@@ -384,6 +384,7 @@ Model::Model(int device, const spi_model_config& cfg, const spi_named_tensor* pa
     os << "bert L" << layers_ << " D" << D_ << " H" << heads_ << " FF" << ffn_ << " S<=" << seq_;
   } else if (family_ == SPI_FAMILY_VIT) {
     mixed_ = cfg.precision == SPI_PREC_F16M;
+    if (const char* e = std::getenv("SPI_QKV_ATTN"); e && *e) qkv_fused_ = std::atoi(e);
     eps_ = cfg.eps > 0 ? cfg.eps : 1e-6f;
     ln_fold_ = ln_fold_enabled(prec_, kVitLnFold);
     heads_ = cfg.num_heads;
@@ -910,7 +911,7 @@ void Model::run_qkv_attention(const LinearW& L, const void* x, const float* in_s
   const int T = B * S, hd = D_ / heads_;
   const float scale = 1.0f / std::sqrt((float)hd);
   const float* mask = w.has_mask ? w.mask_bias : nullptr;
-  if (qkv_fused_ && f16_ && L.prec == Prec::F16 &&
+  if (qkv_fused_ > 0 && S <= (qkv_fused_ >= 2 ? 256 : 128) && f16_ && L.prec == Prec::F16 &&
       qkv_attention_eligible(S, heads_, hd, L.k, L.kpad, L.krep, D_, L.kpad) && (!in_stats || L.c1)) {
     const int nrep = !prof_ ? 1 : op_begin(s, "qkv_attention_S" + std::to_string(S),
                                            2.0 * T * L.n * (double)L.k + 4.0 * B * S * S * D_,
@@ -1246,7 +1247,6 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
       prof_op(s, "vit_assemble", (double)T * D_ * 4 * 3, [&] {
         vit_assemble(static_cast<const float*>(buf[1]), ptr<float>(cls_), ptr<float>(vpos_), x, B, npatch_, D_, s);
       });
-    const float scale = 1.0f / std::sqrt((float)(D_ / heads_));
     if (ln_fold_) {
       // Pre-LN with the LayerNorms folded (ln_fold.hpp) over a two-plane residual stream (round 6,
       // GemmDesc::res_planes): x lives in buf 2 as hi = fp16(x) and lo = fp16(x - hi), a plane of
@@ -1276,11 +1276,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         } else {
           q.in_stats = Sx;
         }
-        run_gemm(L.qkv, i == 0 ? buf[3] : xh, T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s, &q);
-        const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
-                                               (double)T * 4 * D_ * 2);
-        for (int r = 0; r < nrep; ++r) attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
-        if (prof_) op_end(s);
+        run_qkv_attention(L.qkv, i == 0 ? buf[3] : xh, q.in_stats, buf[4], buf[5], B, S, w, s);
         LnSpec o;
         o.out_stats = Sx;
         run_gemm(L.out, buf[5], T, D_, xh, D_, false, Act::None, xh, false, D_, w, s, &o, plane);
@@ -1300,11 +1296,7 @@ void Model::body(Workspace& w, int B, int S_in, hipStream_t s) {
         layernorm(x, D_, ptr<float>(L.ln1.g), ptr<float>(L.ln1.b), f16_ ? nullptr : static_cast<float*>(buf[3]),
                   f16_ ? buf[3] : nullptr, D_, T, D_, eps_, f16_, s);
       });
-      run_gemm(L.qkv, buf[3], T, D_, buf[4], 3 * D_, false, Act::None, nullptr, false, 0, w, s);
-      const int nrep = !prof_ ? 1 : op_begin(s, "attention_S" + std::to_string(S), 4.0 * B * S * S * D_,
-                                             (double)T * 4 * D_ * (f16_ ? 2 : 4));
-      for (int r = 0; r < nrep; ++r) attention(buf[4], nullptr, buf[5], B, S, heads_, D_ / heads_, scale, f16_, s);
-      if (prof_) op_end(s);
+      run_qkv_attention(L.qkv, buf[3], nullptr, buf[4], buf[5], B, S, w, s);
       run_gemm(L.out, buf[5], T, D_, x, D_, true, Act::None, x, true, D_, w, s);
       prof_op(s, "layernorm", ln_bytes(T, false), [&] {
         layernorm(x, D_, ptr<float>(L.ln2.g), ptr<float>(L.ln2.b), f16_ ? nullptr : static_cast<float*>(buf[3]),

@@ -190,7 +190,9 @@ class Model {
   // LayerNorm folded across the GEMMs (fp16, D and FFN multiples of 128; SPI_LN_FOLD=0: the
   // separate LayerNorm launches): no LN launch inside the encoder stack
   bool ln_fold_ = false;
-  bool qkv_fused_ = true;  // SPI_QKV_ATTN=0: the QKV GEMM + attention launches (A/B)
+  // SPI_QKV_ATTN: 0 the QKV GEMM + attention launches (A/B); 1 (default) the fused kernel for S <= 128;
+  // 2 also for 129..256 tokens (ViT-L at 197: correct, but -4 % under the four streams)
+  int qkv_fused_ = 1;
   size_t word_ = 0, pos_ = 0, type0_ = 0;
   LnW emb_ln_, final_ln_;
   std::vector<TfLayer> tf_;
