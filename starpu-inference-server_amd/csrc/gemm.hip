@@ -1675,12 +1675,19 @@ __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) voi
 // Grouped launch (KGroup): 1-D grid, problem-major, then slice, then tile.
 template <int MODE, int BM, int BN, int STAGES, int KIND, int NW = 4>
 __global__ __launch_bounds__(64 * NW, (kMinWaves<BM, BN, STAGES, KIND, NW>)) void gemm_kernel_pair(KGroup g) {
-  int lin = blockIdx.x;
-  const bool second = lin >= g.wgs0;
-  if (second) lin -= g.wgs0;
-  const KArgs& a = second ? g.a[1] : g.a[0];
-  const int kslice = fdiv(lin, a.fd_tiles);
-  gemm_body<MODE, BM, BN, STAGES, KIND, NW>(a, kslice, lin - kslice * a.tiles, lin);
+  // One body per problem (a branch on a workgroup-uniform condition), each with constant kernel
+  // argument offsets: selecting the problem's KArgs by reference had every field become a select of
+  // two loaded values -- SGPR spills to VGPR lanes and the tile decode's FastDiv tables copied to
+  // scratch and read back with a dynamic offset (40 bytes of scratch per lane, round 6)
+  const int lin = blockIdx.x;
+  if (lin >= g.wgs0) {
+    const int l1 = lin - g.wgs0;
+    const int kslice = fdiv(l1, g.a[1].fd_tiles);
+    gemm_body<MODE, BM, BN, STAGES, KIND, NW>(g.a[1], kslice, l1 - kslice * g.a[1].tiles, l1);
+  } else {
+    const int kslice = fdiv(lin, g.a[0].fd_tiles);
+    gemm_body<MODE, BM, BN, STAGES, KIND, NW>(g.a[0], kslice, lin - kslice * g.a[0].tiles, lin);
+  }
 }
 
 struct Plan {
