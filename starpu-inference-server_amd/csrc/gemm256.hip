@@ -252,13 +252,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
 
   // LNC (the LayerNorm consumer fold, RES = 0, ln_in_chunks > 0): the tile rows' {mean, rstd}.
   // Four lanes share a row: lane q of the four loads its 4 of the row's 16 chunk partials (two
-  // 16-byte loads) during the LAST k-tile (ln_load: 8 registers a round, once no DMA is left to
-  // issue), they land under its remaining MFMAs, and the epilogue combines them (ln_combine: Chan's
-  // formula over two xor-shuffle rounds).  Each thread loading its row's 16 partials in the epilogue
-  // (round 4) was a dependent memory round trip plus 32 live registers beside the 128 accumulators:
-  // 84 bytes of spills per lane, ViT-L FFN1 +8 us per launch with the fold (round 6,
-  // tools/loaded_ops.py).  Round h, half-wave lane l = tid & 31: row m0 + kRoundRows h + (tid >> 5)
-  // + 16 (l >> 2) -- the epilogue walk's pass l >> 2 -- chunks 4 (l & 3) .. + 3.
+  // 16-byte loads, ln_load) and the four combine them (ln_combine: Chan's formula over two
+  // xor-shuffle rounds).  Each thread loading its row's 16 partials (round 4) had kept 32 more
+  // registers live beside the 128 accumulators and spilled.  Where the loads go (round 6,
+  // profiles/r06/ln_stats/): 256-row tiles at the epilogue's start -- in the last k-tile, to hide
+  // the round trip, they spilled more (148 bytes per lane against 84) and measured slower (ViT-L
+  // FFN1 35.2 vs 33.1 us back to back, C5 6.77k vs 6.99k); 128-row tiles (64 accumulators) under
+  // the last k-tile's MFMAs (BERT-base's FFN1: C3 +0.8 % against the epilogue start).
+  // Round h, half-wave lane l = tid & 31: row m0 + kRoundRows h + (tid >> 5) + 16 (l >> 2) -- the
+  // epilogue walk's pass l >> 2 -- chunks 4 (l & 3) .. + 3.
   constexpr int kLnRounds = BM / Geo::kRoundRows;
   [[maybe_unused]] floatx4 ln_ch[RES == 0 ? kLnRounds : 1][2];
   [[maybe_unused]] float2 ln_st[RES == 0 ? kLnRounds : 1];
@@ -393,7 +395,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       bar();
       // phase 2
       read_a(buf, 1);
-      if constexpr (R == 0) ln_load();  // fa[0] is dead, nothing left to stage
       if constexpr (R >= 2) stage(0, kt + 2);
       bar();
       mma(1, 0);
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       bar();
       // phase 1
       read_b(buf, 1);
-      if constexpr (R == 0) ln_load();
+      if constexpr (R == 0) ln_load();  // (128-row tiles: under the last k-tile's MFMAs)
       if constexpr (R >= 2) stage(2, kt + 2);
       if constexpr (R >= 1)
         vm_wait_nolgkm<2 * (1 + (R >= 2 ? 3 : 0))>();
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
       mma(0, 0);
       bar();
       read_b(buf, 1);
-      if constexpr (R == 0) ln_load();
+      if constexpr (R == 0) ln_load();  // (128-row tiles: under the last k-tile's MFMAs)
       if constexpr (R >= 1) stage(2, kt + 1);
       if constexpr (R >= 1)
         vm_wait_nolgkm<2>();
@@ -649,8 +650,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const G256Args g) {
     constexpr bool LNO = decltype(lno_c)::value;
     constexpr int kRR = Geo::kRoundRows, kRounds = BM / kRR, kPasses = kRR / 16;  // rounds of the LDS-parked tile
     [[maybe_unused]] float c18[8];
-    if constexpr (LNC) {  // the rows' {mean, rstd} (ln_st) from the partials the last k-tile loaded
+    if constexpr (LNC) {  // the rows' {mean, rstd} (ln_st)
       static_assert(kRounds == kLnRounds, "epilogue rounds");
+      if constexpr (BM == 256) ln_load();  // (128-row tiles loaded them in the last k-tile)
       ln_combine();
       const floatx4 c0 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb);
       const floatx4 c1 = *reinterpret_cast<const floatx4*>(g.ln_c1 + nb + 4);
