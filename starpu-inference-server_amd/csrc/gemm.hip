@@ -1759,10 +1759,17 @@ struct Knobs {
 constexpr int kHaloStages = 3;     // W ring of the halo kinds
 constexpr int kHaloMinH = 14;      // 7x7 maps: the implicit GEMM measured faster (77 % row use)
 constexpr int kHaloMaxTiles = 64;  // halo only when the implicit GEMM has fewer 64x64 tiles
-#ifndef SPI_ST3_MIN  // variant builds (tools/build_variant.sh ... -DSPI_ST3_MIN=N) for ring-depth A/Bs
-#define SPI_ST3_MIN 16
+// Ring depth by k-steps per slice (variant builds: tools/build_variant.sh ... -DSPI_ST3_MIN=N /
+// -DSPI_ST4_MIN=N).  Round 6: 3 stages from 12 k-steps, no 4-stage ring -- BERT-base's out-proj (12
+// k-steps, was 2 stages) and FFN2 (48, was 4: +2.4 % in round 3) then share one kernel instance:
+// C3 +1.2 %, each change alone +0.2 %; C2 / C4 +-0.3 % (profiles/r06/ring_depth/)
+#ifndef SPI_ST3_MIN
+#define SPI_ST3_MIN 12
 #endif
-constexpr int kSt3Min = SPI_ST3_MIN, kSt4Min = 32;  // ring depth by k-steps per slice (4 stages: BERT FFN2 +2.4 %)
+#ifndef SPI_ST4_MIN
+#define SPI_ST4_MIN (1 << 30)
+#endif
+constexpr int kSt3Min = SPI_ST3_MIN, kSt4Min = SPI_ST4_MIN;
 
 Knobs read_knobs() {
   Knobs k;
