@@ -289,6 +289,76 @@ __global__ __launch_bounds__(256) void layernorm_planes_kernel(const _Float16* x
                  lane);
 }
 
+// The same for D = NV * 256 (BERT-base 768, ViT-L 1024): lane l holds NV groups of 4 columns
+// (c = 4 (64 j + l)), read as 8-byte hi and lo vectors -- the vector form of layernorm_vec_kernel
+// (round 6: the scalar planes kernel ran BERT's output LayerNorm in 10.3 us against 4.6 for the
+// fp32 vector one).
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void layernorm_planes_vec_kernel(const _Float16* __restrict__ xh, size_t plane,
+                                                                   int ldx, const float* __restrict__ g,
+                                                                   const float* __restrict__ b, float* yf, T* yt,
+                                                                   int ldy, int rows, float eps) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = NV * 256;
+  const half4* xr = reinterpret_cast<const half4*>(xh + (size_t)row * ldx);
+  const half4* lr = reinterpret_cast<const half4*>(xh + (size_t)row * ldx + plane);
+  half4 hv[NV], lv[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    hv[j] = xr[j * 64 + lane];
+    lv[j] = lr[j * 64 + lane];
+  }
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4 gg[NV], bb[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    gg[j] = g4[j * 64 + lane];
+    bb[j] = b4[j * 64 + lane];
+  }
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[j][e] = static_cast<float>(hv[j][e]) + static_cast<float>(lv[j][e]);
+      s += v[j][e];
+    }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += (v[j][e] - mean) * (v[j][e] - mean);
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c4 = j * 64 + lane;
+    float4 o;
+    o.x = (v[j][0] - mean) * rstd * gg[j].x + bb[j].x;
+    o.y = (v[j][1] - mean) * rstd * gg[j].y + bb[j].y;
+    o.z = (v[j][2] - mean) * rstd * gg[j].z + bb[j].z;
+    o.w = (v[j][3] - mean) * rstd * gg[j].w + bb[j].w;
+    if (yf) reinterpret_cast<float4*>(yf + (size_t)row * ldy)[c4] = o;
+    if (yt) {
+      if constexpr (sizeof(T) == 2) {
+        half4 h;
+        h[0] = static_cast<_Float16>(o.x);
+        h[1] = static_cast<_Float16>(o.y);
+        h[2] = static_cast<_Float16>(o.z);
+        h[3] = static_cast<_Float16>(o.w);
+        reinterpret_cast<half4*>(yt + (size_t)row * ldy)[c4] = h;
+      } else {
+        reinterpret_cast<float4*>(yt + (size_t)row * ldy)[c4] = o;
+      }
+    }
+  }
+}
+
 // LayerNorm rows of D = NV * 256: one wave per row, every lane holds NV float4
 // column groups (c = 4 * (64 j + lane)), so the row moves as 16-byte loads and
 // stores (fp16 copies as 8-byte stores) -- a quarter of the scalar kernel's
@@ -374,6 +444,73 @@ __global__ __launch_bounds__(256) void bert_embed_kernel(
   }
   ln_row<T, VPL>(v, D, g, b, eps, yf + (size_t)row * D, yt ? yt + (size_t)row * D : nullptr,
                  lane);
+}
+
+// The same for D = NV * 256 with 16-byte gathers: lane l holds NV groups of 4 columns
+// (c = 4 (64 j + l)) -- a quarter of the scalar kernel's memory instructions (round 6: BERT-base's
+// embedding ran 14.6 us in the loop trace, 1.7 % of C3).
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void bert_embed_vec_kernel(const int64_t* ids, const float* __restrict__ word,
+                                                             const float* __restrict__ pos,
+                                                             const float* __restrict__ type0,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ b, float* yf, T* yt, int B,
+                                                             int S, int vocab, float eps) {
+  constexpr int D = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B * S) return;
+  const int s = row % S;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const float4* w4 = reinterpret_cast<const float4*>(word + (size_t)id * D);
+  const float4* p4 = reinterpret_cast<const float4*>(pos + (size_t)s * D);
+  const float4* t4 = reinterpret_cast<const float4*>(type0);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  float4 v[NV], gg[NV], bb[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c4 = j * 64 + lane;
+    const float4 w = w4[c4], t = t4[c4], p = p4[c4];
+    v[j] = float4{(w.x + t.x) + p.x, (w.y + t.y) + p.y, (w.z + t.z) + p.z, (w.w + t.w) + p.w};
+    gg[j] = g4[c4];
+    bb[j] = b4[c4];
+  }
+  float sm = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  const float mean = wave_sum(sm) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float a0 = v[j].x - mean, a1 = v[j].y - mean, a2 = v[j].z - mean, a3 = v[j].w - mean;
+    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c4 = j * 64 + lane;
+    float4 o;
+    o.x = (v[j].x - mean) * rstd * gg[j].x + bb[j].x;
+    o.y = (v[j].y - mean) * rstd * gg[j].y + bb[j].y;
+    o.z = (v[j].z - mean) * rstd * gg[j].z + bb[j].z;
+    o.w = (v[j].w - mean) * rstd * gg[j].w + bb[j].w;
+    reinterpret_cast<float4*>(yf + (size_t)row * D)[c4] = o;
+    if (yt) {
+      if constexpr (sizeof(T) == 2) {
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        half4 h;
+        h[0] = static_cast<_Float16>(o.x);
+        h[1] = static_cast<_Float16>(o.y);
+        h[2] = static_cast<_Float16>(o.z);
+        h[3] = static_cast<_Float16>(o.w);
+        reinterpret_cast<half4*>(yt + (size_t)row * D)[c4] = h;
+      } else {
+        reinterpret_cast<float4*>(yt + (size_t)row * D)[c4] = o;
+      }
+    }
+  }
 }
 
 __global__ void mask_bias_kernel(const int64_t* mask, float* bias, int n) {
@@ -555,6 +692,23 @@ void bert_embed(const int64_t* ids, const float* word, const float* pos, const f
                 const float* g, const float* b, float* yf, void* yt, int B, int S, int D,
                 int vocab, float eps, bool f16, hipStream_t s) {
   const dim3 grid((B * S + 3) / 4);
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if ((D == 768 || D == 1024) && al16(word) && al16(pos) && al16(type0) && al16(g) && al16(b) && al16(yf) &&
+      (!yt || (reinterpret_cast<uintptr_t>(yt) & (f16 ? 7 : 15)) == 0)) {
+    if (D == 768 && f16)
+      SPI_LAUNCH((bert_embed_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
+                 (_Float16*)yt, B, S, vocab, eps);
+    else if (D == 768)
+      SPI_LAUNCH((bert_embed_vec_kernel<float, 3>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
+                 (float*)yt, B, S, vocab, eps);
+    else if (f16)
+      SPI_LAUNCH((bert_embed_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
+                 (_Float16*)yt, B, S, vocab, eps);
+    else
+      SPI_LAUNCH((bert_embed_vec_kernel<float, 4>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
+                 (float*)yt, B, S, vocab, eps);
+    return;
+  }
   if (f16)
     SPI_LAUNCH((bert_embed_kernel<_Float16>), grid, dim3(256), 0, s, ids, word, pos,
                        type0, g, b, yf, (_Float16*)yt, B, S, D, vocab, eps);
@@ -597,6 +751,23 @@ void layernorm_planes(const _Float16* xh, size_t plane, int ldx, const float* g,
                       int ldy, int rows, int D, float eps, bool f16, hipStream_t s) {
   if (D > 1024) throw std::invalid_argument("layernorm_planes: D <= 1024");
   const dim3 grid((rows + 3) / 4);
+  const auto al = [](const void* q, uintptr_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+  if ((D == 768 || D == 1024) && ldx % 4 == 0 && plane % 4 == 0 && ldy % 4 == 0 && al(xh, 8) && al(g, 16) &&
+      al(b, 16) && (!yf || al(yf, 16)) && (!yt || al(yt, f16 ? 8 : 16))) {
+    if (D == 768 && f16)
+      SPI_LAUNCH((layernorm_planes_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf,
+                 (_Float16*)yt, ldy, rows, eps);
+    else if (D == 768)
+      SPI_LAUNCH((layernorm_planes_vec_kernel<float, 3>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf, (float*)yt,
+                 ldy, rows, eps);
+    else if (f16)
+      SPI_LAUNCH((layernorm_planes_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf,
+                 (_Float16*)yt, ldy, rows, eps);
+    else
+      SPI_LAUNCH((layernorm_planes_vec_kernel<float, 4>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf, (float*)yt,
+                 ldy, rows, eps);
+    return;
+  }
   if (f16)
     SPI_LAUNCH((layernorm_planes_kernel<_Float16>), grid, dim3(256), 0, s, xh, plane, ldx, g, b, yf, (_Float16*)yt,
                ldy, rows, D, eps);
