@@ -426,11 +426,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void bert_embed_kernel(
     const int64_t* ids, const float* word, const float* pos, const float* type0,
     const float* g, const float* b, float* yf, T* yt, int B, int S, int D, int vocab,
-    float eps) {
+    float eps, const int64_t* mask, float* mask_bias) {
   constexpr int VPL = 16;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B * S) return;
+  if (mask && lane == 0) mask_bias[row] = mask[row] != 0 ? 0.f : -3.4028234663852886e38f;
   const int s = row % S;
   int64_t id = ids[row];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
@@ -455,11 +456,14 @@ __global__ __launch_bounds__(256) void bert_embed_vec_kernel(const int64_t* ids,
                                                              const float* __restrict__ type0,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ b, float* yf, T* yt, int B,
-                                                             int S, int vocab, float eps) {
+                                                             int S, int vocab, float eps, const int64_t* mask,
+                                                             float* mask_bias) {
   constexpr int D = NV * 256;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B * S) return;
+  // the attention's additive key bias of this token, (1 - m) * finfo(f32).min (mask_bias_kernel's)
+  if (mask && lane == 0) mask_bias[row] = mask[row] != 0 ? 0.f : -3.4028234663852886e38f;
   const int s = row % S;
   int64_t id = ids[row];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
@@ -690,31 +694,31 @@ void layernorm(const float* x, int ldx, const float* g, const float* b, float* y
 
 void bert_embed(const int64_t* ids, const float* word, const float* pos, const float* type0,
                 const float* g, const float* b, float* yf, void* yt, int B, int S, int D,
-                int vocab, float eps, bool f16, hipStream_t s) {
+                int vocab, float eps, bool f16, hipStream_t s, const int64_t* mask, float* mask_bias) {
   const dim3 grid((B * S + 3) / 4);
   const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if ((D == 768 || D == 1024) && al16(word) && al16(pos) && al16(type0) && al16(g) && al16(b) && al16(yf) &&
       (!yt || (reinterpret_cast<uintptr_t>(yt) & (f16 ? 7 : 15)) == 0)) {
     if (D == 768 && f16)
       SPI_LAUNCH((bert_embed_vec_kernel<_Float16, 3>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
-                 (_Float16*)yt, B, S, vocab, eps);
+                 (_Float16*)yt, B, S, vocab, eps, mask, mask_bias);
     else if (D == 768)
       SPI_LAUNCH((bert_embed_vec_kernel<float, 3>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
-                 (float*)yt, B, S, vocab, eps);
+                 (float*)yt, B, S, vocab, eps, mask, mask_bias);
     else if (f16)
       SPI_LAUNCH((bert_embed_vec_kernel<_Float16, 4>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
-                 (_Float16*)yt, B, S, vocab, eps);
+                 (_Float16*)yt, B, S, vocab, eps, mask, mask_bias);
     else
       SPI_LAUNCH((bert_embed_vec_kernel<float, 4>), grid, dim3(256), 0, s, ids, word, pos, type0, g, b, yf,
-                 (float*)yt, B, S, vocab, eps);
+                 (float*)yt, B, S, vocab, eps, mask, mask_bias);
     return;
   }
   if (f16)
     SPI_LAUNCH((bert_embed_kernel<_Float16>), grid, dim3(256), 0, s, ids, word, pos,
-                       type0, g, b, yf, (_Float16*)yt, B, S, D, vocab, eps);
+                       type0, g, b, yf, (_Float16*)yt, B, S, D, vocab, eps, mask, mask_bias);
   else
     SPI_LAUNCH((bert_embed_kernel<float>), grid, dim3(256), 0, s, ids, word, pos,
-                       type0, g, b, yf, (float*)yt, B, S, D, vocab, eps);
+                       type0, g, b, yf, (float*)yt, B, S, D, vocab, eps, mask, mask_bias);
 }
 
 void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s) {

@@ -1087,15 +1087,15 @@ void Model::prologue(Workspace& w, int B, int S, const void* const* in, hipStrea
     if (prof_) op_end(s);
   } else if (family_ == SPI_FAMILY_BERT) {
     const double T = (double)B * S;
-    prof_op(s, "bert_embed", T * D_ * (4 * 3 + 4 + (f16_ ? 2 : 0)), [&] {
+    // the attention mask's additive bias is written by the embedding kernel (round 6: one launch
+    // fewer per forward than a separate mask_to_bias)
+    w.has_mask = in[1] != nullptr;
+    prof_op(s, "bert_embed", T * D_ * (4 * 3 + 4 + (f16_ ? 2 : 0)) + (w.has_mask ? T * 12 : 0), [&] {
       bert_embed(static_cast<const int64_t*>(in[0]), ptr<float>(word_), ptr<float>(pos_), ptr<float>(type0_),
                  ptr<float>(emb_ln_.g), ptr<float>(emb_ln_.b), static_cast<float*>(w.bufs[0]),
-                 f16_ ? w.bufs[1] : nullptr, B, S, D_, vocab_, eps_, f16_, s);
+                 f16_ ? w.bufs[1] : nullptr, B, S, D_, vocab_, eps_, f16_, s,
+                 w.has_mask ? static_cast<const int64_t*>(in[1]) : nullptr, w.has_mask ? w.mask_bias : nullptr);
     });
-    w.has_mask = in[1] != nullptr;
-    if (w.has_mask)
-      prof_op(s, "mask_to_bias", T * 12,
-              [&] { mask_to_bias(static_cast<const int64_t*>(in[1]), w.mask_bias, B * S, s); });
   } else if (family_ == SPI_FAMILY_VIT) {
     prof_op(s, "patchify", (double)B * 3 * image_ * image_ * (4 + (f16_ ? 2 : 4)),
             [&] { patchify(static_cast<const float*>(in[0]), w.bufs[0], B, 3, image_, image_, patch_, f16_, s); });

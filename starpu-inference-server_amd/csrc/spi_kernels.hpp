@@ -199,11 +199,12 @@ void avgpool_nhwc_split(const void* x, float* y, int B, int HW, int C, hipStream
 void layernorm(const float* x, int ldx, const float* g, const float* b,
                float* yf, void* yt, int ldy, int rows, int D, float eps, bool f16,
                hipStream_t s);
-// BERT embeddings: LN(word[ids] + pos[s] + type[0]) -> fp32 + compute type.
+// BERT embeddings: LN(word[ids] + pos[s] + type[0]) -> fp32 + compute type; with a mask, each
+// token's additive attention bias too (mask_to_bias's, one launch fewer per forward).
 void bert_embed(const int64_t* ids, const float* word, const float* pos,
                 const float* type0, const float* g, const float* b, float* yf,
                 void* yt, int B, int S, int D, int vocab, float eps, bool f16,
-                hipStream_t s);
+                hipStream_t s, const int64_t* mask = nullptr, float* mask_bias = nullptr);
 // int64 attention mask [B,S] -> additive fp32 bias [B,S] (0 or finfo.min).
 void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s);
 // ViT: NCHW fp32 image -> patch rows [B*P, C*ps*ps] (compute type).
