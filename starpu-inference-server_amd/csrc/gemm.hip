@@ -1718,6 +1718,9 @@ int estep_of(Prec prec) {
 struct Knobs {
   bool forced = false;
   Plan plan{};
+  // SPI_GEMM_PLAN_LONGK="K,bm,bn,stages,splits": that plan for dense GEMMs with K >= K only (A/B sweeps)
+  int longk_plan_k = 0;
+  Plan longk_plan{};
   int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
   int max_split = 0;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
@@ -1781,6 +1784,17 @@ Knobs read_knobs() {
       if (ok_tile && ok_st && sp >= 1) {
         k.forced = true;
         k.plan = Plan{bm, bn, st, sp, 0};
+      }
+    }
+  }
+  if (const char* e = std::getenv("SPI_GEMM_PLAN_LONGK"); e && *e) {
+    int kk = 0, bm = 0, bn = 0, st = 0, sp = 0;
+    if (std::sscanf(e, "%d,%d,%d,%d,%d", &kk, &bm, &bn, &st, &sp) == 5) {
+      const bool ok_tile = (bm == 128 && bn == 128) || (bm == 128 && bn == 64) || (bm == 64 && bn == 64);
+      const bool ok_st = st >= 2 && st <= 4 && !(bm == 128 && bn == 128 && st > 2) && !(bm == 128 && bn == 64 && st > 3);
+      if (ok_tile && ok_st && sp >= 1 && kk > 0) {
+        k.longk_plan_k = kk;
+        k.longk_plan = Plan{bm, bn, st, sp, 0};
       }
     }
   }
@@ -1990,6 +2004,8 @@ Plan choose_plan(const GemmDesc& d, Prec prec) {
   const int ES = estep_of(prec);
   const int ksteps = d.Kpad / ES;
   if (k.forced) return finish_plan(k.plan, ksteps, ES, d.krep);
+  if (k.longk_plan_k > 0 && !d.conv && !d.pool_rows && d.K >= k.longk_plan_k)
+    return finish_plan(k.longk_plan, ksteps, ES, d.krep);
   const auto tiles_of = [&](int bm, int bn) { return ((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn); };
   // a deeper ring pays only on long K loops (4 stages only reach the 64x64 tiles, finish_plan caps the others)
   const auto stages_for = [](int kt) { return kt >= kSt4Min ? 4 : kt >= kSt3Min ? 3 : 2; };

@@ -21,7 +21,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 KNOBS = ["SPI_STEM_FUSED", "SPI_GEMM_256_MIN", "SPI_GEMM_256_LONGK", "SPI_GEMM_HALO_CFG", "SPI_GEMM_WIN",
-         "SPI_GEMM_MAXSPLIT", "SPI_GEMM_PLAN", "SPI_CONV_WRES", "SPI_LN_FOLD", "SPI_QKV_ATTN", "SPI_GEMM_256_ORDER"]
+         "SPI_GEMM_MAXSPLIT", "SPI_GEMM_PLAN", "SPI_CONV_WRES", "SPI_LN_FOLD", "SPI_QKV_ATTN", "SPI_GEMM_256_ORDER", "SPI_GEMM_PLAN_LONGK"]
 
 
 def parse(p):
