@@ -219,7 +219,11 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv,
 // O^T's accumulator holds 4 consecutive head dims of one query per lane: 8-byte stores.
 // NW waves per workgroup = 16 NW query rows: 4 (BERT) or 8 (ViT's S = 197: the K / V tiles are
 // staged once per 128 queries instead of per 64; 2 query tiles per head instead of 4).
-template <int NW>
+// SK > 0 (round 6, S <= SK): the whole sequence's K and V are staged once (SK rows, zero past
+// S) behind one barrier, and the key-tile loop runs with no barrier and no global load: ViT's
+// four 64-key tiles no longer pay a load-latency + barrier round trip each.  NW = 16 with SK: one
+// workgroup per (batch, head), so K / V are read once per head.
+template <int NW, int SK>
 __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float16* __restrict__ qkv,
                                                                const float* __restrict__ mask_bias,
                                                                _Float16* __restrict__ ctx, int S, int H,
@@ -228,8 +232,9 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
   typedef short short4v __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) short4v lds_s4;
   constexpr int LD = HD + 8;  // K / V row stride in elements (144 B: 16-byte rows, 8-byte tr reads)
-  __shared__ __attribute__((aligned(16))) _Float16 Ks[KT * LD];
-  __shared__ __attribute__((aligned(16))) _Float16 Vs[KT * LD];
+  constexpr int KR = SK ? SK : KT;  // staged key rows
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[KR * LD];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[KR * LD];
 
   const int D = H * HD, ld = 3 * D;
   const int b = blockIdx.y / H, h = blockIdx.y % H;
@@ -253,7 +258,7 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
 #pragma unroll
   for (int d = 0; d < 4; ++d) o[d] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int NCH = KT * HD / 8 / NT;  // 16-byte chunks of K (and of V) per thread per tile
+  constexpr int NCH = KT * HD / 8 / NT > 0 ? KT * HD / 8 / NT : 1;  // 16-byte chunks of K (and V) per thread per tile
   uint4 kreg[NCH], vreg[NCH];
   auto fetch = [&](int k0) {
 #pragma unroll
@@ -272,18 +277,48 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
   // head-dim block dblk: row 32 s + 16 t + 4 fq + fr / 4, columns 16 dblk + 4 (fr % 4)
   const int tr_off = ((4 * fq + (fr >> 2)) * LD + 4 * (fr & 3)) * 2;
   const bool live = q0 + wave * 16 < S;  // wave-uniform
-  fetch(0);
-  for (int k0 = 0; k0 < S; k0 += KT) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous tile's reads are done
+  if constexpr (SK > 0) {
+    // the whole sequence: SK * 8 16-byte chunks of K and of V, rows past S zero (V's rows
+    // past S meet P = 0 in the last 32-key step, so they must be finite)
+    constexpr int NW_CH = (SK * (HD / 8) + NT - 1) / NT;
+    uint4 kw[NW_CH], vw[NW_CH];
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
+    for (int i = 0; i < NW_CH; ++i) {
       const int c = tid + i * NT;
       const int key = c / (HD / 8), dc = c % (HD / 8);
-      *reinterpret_cast<uint4*>(Ks + key * LD + dc * 8) = kreg[i];
-      *reinterpret_cast<uint4*>(Vs + key * LD + dc * 8) = vreg[i];
+      kw[i] = vw[i] = make_uint4(0, 0, 0, 0);
+      if (key < S) {
+        kw[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + D + h * HD + dc * 8);
+        vw[i] = *reinterpret_cast<const uint4*>(base + (size_t)key * ld + 2 * D + h * HD + dc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NW_CH; ++i) {
+      const int c = tid + i * NT;
+      const int key = c / (HD / 8), dc = c % (HD / 8);
+      if (key < SK) {
+        *reinterpret_cast<uint4*>(Ks + key * LD + dc * 8) = kw[i];
+        *reinterpret_cast<uint4*>(Vs + key * LD + dc * 8) = vw[i];
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (k0 + KT < S) fetch(k0 + KT);
+    if (!live) return;  // no barrier follows
+  } else {
+    fetch(0);
+  }
+  for (int k0 = 0; k0 < S; k0 += KT) {
+    if constexpr (SK == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous tile's reads are done
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int c = tid + i * NT;
+        const int key = c / (HD / 8), dc = c % (HD / 8);
+        *reinterpret_cast<uint4*>(Ks + key * LD + dc * 8) = kreg[i];
+        *reinterpret_cast<uint4*>(Vs + key * LD + dc * 8) = vreg[i];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (k0 + KT < S) fetch(k0 + KT);
+    }
 
     // A wave whose 16 queries all lie past S (ViT's last query tile: 5 of 64 rows) only
     // stages; key blocks past S skip their MFMAs (their scores are -inf through the bias, so
@@ -291,6 +326,7 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
     // transposed reads).
     if (!live) continue;
     const int kleft = S - k0;
+    const int kb = SK ? k0 : 0;  // the tile's first staged row
     // S^T: sacc[j][r] = score of key k0 + 16 j + 4 fq + r for query fr
     floatx4 sacc[4];
 #pragma unroll
@@ -299,7 +335,7 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
       if (j * 16 < kleft) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const half8 kf = *reinterpret_cast<const half8*>(Ks + (j * 16 + fr) * LD + s * 32 + fq * 8);
+          const half8 kf = *reinterpret_cast<const half8*>(Ks + (kb + j * 16 + fr) * LD + s * 32 + fq * 8);
           sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[s], sacc[j], 0, 0, 0);
         }
       }
@@ -337,7 +373,8 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
 
     // O^T += V^T P^T
-    __attribute__((address_space(3))) char* vb = (__attribute__((address_space(3))) char*)Vs + tr_off;
+    __attribute__((address_space(3))) char* vb =
+        (__attribute__((address_space(3))) char*)Vs + tr_off + kb * LD * 2;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (s * 32 >= kleft) break;
@@ -367,7 +404,19 @@ __global__ __launch_bounds__(64 * NW) void attn_f16_swapped_kernel(const _Float1
 
 }  // namespace
 
-void attention_reload_env() {}
+// SPI_ATTN_WHOLE (S in 129..224): 2 (default) one 16-wave workgroup per (batch, head), 1 two 8-wave
+// workgroups per head, both staging the whole K / V once; 0 the per-tile staging.  ViT-L under the
+// four streams: 2 +1.4 %, 1 +0.6 % over 0 (profiles/r06/attn_whole/)
+static int g_attn_whole = -1;
+static int attn_knobs_whole() {
+  if (g_attn_whole < 0) {
+    const char* e = std::getenv("SPI_ATTN_WHOLE");
+    g_attn_whole = (e && *e) ? std::atoi(e) : 2;
+  }
+  return g_attn_whole;
+}
+
+void attention_reload_env() { g_attn_whole = -1; }
 
 // fp16: the swapped orientation, 8-wave workgroups of 128 queries for S > 128 (ViT-L's 197),
 // 4 waves of 64 queries otherwise; fp32: the round-2 orientation (the round-2 fp16 kernel
@@ -381,10 +430,20 @@ void attention(const void* qkv, const float* mask_bias, void* ctx, int B, int S,
 #endif
   if (f16 && S >= SPI_ATTN_S8_MIN) {
     const dim3 g8((S + 127) / 128, B * heads);
-    SPI_LAUNCH(attn_f16_swapped_kernel<8>, g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
-                       (_Float16*)ctx, S, heads, scale);
+    // whole-sequence staging up to 224 keys (64.5 KiB: two workgroups per CU), tiles beyond;
+    // the 16-wave form stages K / V once per head instead of once per 128 queries
+    const int whole = attn_knobs_whole();
+    if (whole == 2 && S <= 224)  // one 16-wave workgroup per (batch, head): K / V staged once per head
+      SPI_LAUNCH((attn_f16_swapped_kernel<16, 224>), dim3((S + 255) / 256, B * heads), dim3(1024), 0, s,
+                 (const _Float16*)qkv, mask_bias, (_Float16*)ctx, S, heads, scale);
+    else if (whole && S <= 224)
+      SPI_LAUNCH((attn_f16_swapped_kernel<8, 224>), g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
+                 (_Float16*)ctx, S, heads, scale);
+    else
+      SPI_LAUNCH((attn_f16_swapped_kernel<8, 0>), g8, dim3(512), 0, s, (const _Float16*)qkv, mask_bias,
+                 (_Float16*)ctx, S, heads, scale);
   } else if (f16) {
-    SPI_LAUNCH(attn_f16_swapped_kernel<4>, grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
+    SPI_LAUNCH((attn_f16_swapped_kernel<4, 0>), grid, dim3(256), 0, s, (const _Float16*)qkv, mask_bias,
                        (_Float16*)ctx, S, heads, scale);
   } else {
     SPI_LAUNCH((attn_kernel<float>), grid, dim3(256), 0, s, (const float*)qkv,

@@ -5,6 +5,8 @@ Tolerances are normalised max-abs error (max|got - ref| / max|ref|):
 fp32 (exact fp32 MFMA FMA chains) 1e-5; fp16x3 (split fp16) 1e-5; fp16 (fp16
 operands rounded from the fp32 reference inputs, fp32 accumulation) 5e-3.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -84,7 +86,8 @@ def test_conv2d_nhwc(ops, prec, B, H, cin, cout, k, stride):
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 @pytest.mark.parametrize("B,S,heads,masked", [(2, 128, 12, False), (3, 80, 4, True), (2, 197, 16, False),
                                               (1, 5, 2, False), (2, 64, 2, True), (2, 197, 3, True),
-                                              (8, 128, 12, True)])
+                                              (8, 128, 12, True), (2, 224, 3, True), (1, 225, 2, True),
+                                              (2, 129, 2, True), (1, 161, 2, False)])
 def test_attention(ops, prec, B, S, heads, masked):
     g = torch.Generator().manual_seed(B * S + heads)
     D = heads * 64
@@ -102,6 +105,27 @@ def test_attention(ops, prec, B, S, heads, masked):
     err = normalized_max_error(ctx.float().cpu().numpy(), ref.numpy())
     tol = 1e-5 if prec == "fp32" else 3e-3
     assert err < tol, f"{prec} attention B{B} S{S} H{heads}: {err:.3e}"
+
+
+@pytest.mark.parametrize("S", [129, 197, 224])
+def test_attention_whole_sequence_staging_matches_tiles(ops, S):
+    """Round 6: for 128 < S <= 224 the fp16 kernel stages the whole K / V once (SPI_ATTN_WHOLE=2,
+    default: one 16-wave workgroup per head; =1 two 8-wave ones); the per-tile staging (=0) runs the same arithmetic in the same order: bit-identical."""
+    B, heads = 2, 3
+    g = torch.Generator().manual_seed(S)
+    qkv = (torch.randn(B * S, 3 * heads * 64, generator=g) * 1.5).half().cuda()
+    bias = torch.zeros(B, S)
+    bias[1, S - 7:] = torch.finfo(torch.float32).min
+    outs = {}
+    try:
+        for whole in ("1", "2", "0"):
+            os.environ["SPI_ATTN_WHOLE"] = whole
+            ops.lib.spi_debug_gemm_reload_env()
+            outs[whole] = ops.attention("fp16", qkv, B, S, heads, mask_bias=bias.cuda()).cpu()
+    finally:
+        os.environ.pop("SPI_ATTN_WHOLE", None)
+        ops.lib.spi_debug_gemm_reload_env()
+    assert torch.equal(outs["1"], outs["0"]) and torch.equal(outs["2"], outs["0"])
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
