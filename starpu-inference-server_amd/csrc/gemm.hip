@@ -1711,7 +1711,7 @@ int estep_of(Prec prec) {
 // 128x128 rings, 4-stage halo rings, XCD-local split-K, per-knob ring depths,
 // DESIGN.md 6) are gone; what remains:
 //   SPI_GEMM_PLAN="bm,bn,stages,splits"  force one plan for every GEMM (sweeps)
-//   SPI_GEMM_MAXSPLIT=S                  cap split-K (1: none)
+//   SPI_GEMM_MAXSPLIT=S                  cap split-K (default 8; 1: none, 0: uncapped)
 //   SPI_GEMM_HALO_CFG                    halo candidates: "0" off, "rows,a|s" forced,
 //                                        "OW:rows,a|s;..." per map width
 //   SPI_GEMM_256_MIN / SPI_GEMM_256_LONGK  gemm256 routing (below)
@@ -1722,7 +1722,9 @@ struct Knobs {
   int longk_plan_k = 0;
   Plan longk_plan{};
   int target = 128;  // round 3 (with the joint pair plan): ResNet-18 fp16m +2 % over 192, BERT / ResNet-152 +-0
-  int max_split = 0;
+  // split-K cap: ResNet-18 bs1 (layer 4: 12 slices, layer 3: 4) +1.8 % at 8 or 6 over uncapped,
+  // bs8 +-0.5 % (no conv splits past 6 there); round 6, profiles/r06/maxsplit/
+  int max_split = 8;
   int halo = 1;  // 3x3/s1 convs from LDS-resident input bands (kConvHalo)
   // SPI_GEMM_WIN=0: 3x3/s1 tap walks without the kw window (kConvTapW); 2 / 3: 64 x 64 window
   // tiles as two K groups of 4 waves (8-wave workgroups), at the 4-wave plan's slices / half of them
@@ -1839,7 +1841,7 @@ Knobs read_knobs() {
     }
   }
   if (const char* e = std::getenv("SPI_GEMM_256_ORDER"); e && *e) k.g256_order = std::max(-1, std::min(1, std::atoi(e)));
-  if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("SPI_GEMM_MAXSPLIT"); e && *e) k.max_split = std::max(0, std::atoi(e));  // 0: uncapped
   if (const char* e = std::getenv("SPI_GEMM_WIN"); e && *e) k.win = std::max(0, std::min(3, std::atoi(e)));
   return k;
 }
