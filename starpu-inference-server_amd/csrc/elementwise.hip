@@ -542,6 +542,37 @@ __global__ void patchify_kernel(const float* __restrict__ x, T* __restrict__ y, 
   }
 }
 
+// Vector form (round 6; ps % 8 == 0, W % 4 == 0, 16-byte aligned x / y): one thread per 8
+// consecutive kw of one (patch row, c, kh): two 16-byte loads, one 16-byte (fp16) or two (fp32)
+// stores; consecutive threads write consecutive y chunks.  32-bit index math (host-checked).
+template <typename T>
+__global__ __launch_bounds__(256) void patchify_vec_kernel(const float* __restrict__ x, T* __restrict__ y, int C,
+                                                           int H, int W, int ps, int GH, int GW, int n) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int segs = ps >> 3;
+  const int seg = t % segs;
+  int r = t / segs;
+  const int kh = r % ps;
+  r /= ps;
+  const int c = r % C;
+  const int row = r / C;  // (b, ph, pw)
+  const int pw = row % GW, ph = (row / GW) % GH, b = row / (GW * GH);
+  const float4* src =
+      reinterpret_cast<const float4*>(x + ((size_t)(b * C + c) * H + ph * ps + kh) * W + pw * ps + seg * 8);
+  const float4 v0 = src[0], v1 = src[1];
+  T* dst = y + (size_t)row * (C * ps * ps) + (c * ps + kh) * ps + seg * 8;
+  if constexpr (sizeof(T) == 2) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 o = {(_Float16)v0.x, (_Float16)v0.y, (_Float16)v0.z, (_Float16)v0.w,
+                  (_Float16)v1.x, (_Float16)v1.y, (_Float16)v1.z, (_Float16)v1.w};
+    *reinterpret_cast<h8*>(dst) = o;
+  } else {
+    reinterpret_cast<float4*>(dst)[0] = v0;
+    reinterpret_cast<float4*>(dst)[1] = v1;
+  }
+}
+
 __global__ void vit_assemble_kernel(const float* __restrict__ patches,
                                     const float* __restrict__ cls,
                                     const float* __restrict__ pos, float* __restrict__ x,
@@ -728,6 +759,18 @@ void mask_to_bias(const int64_t* mask, float* bias, int n, hipStream_t s) {
 void patchify(const float* x, void* y, int B, int C, int H, int W, int ps, bool f16,
               hipStream_t s) {
   const size_t n = (size_t)B * C * H * W;
+  const auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (ps % 8 == 0 && W % 4 == 0 && n / 8 < (size_t)INT32_MAX && n < (size_t)INT32_MAX && al16(x) && al16(y)) {
+    const int GH = H / ps, GW = W / ps;
+    const int nt = B * GH * GW * C * ps * (ps / 8);
+    if (f16)
+      SPI_LAUNCH((patchify_vec_kernel<_Float16>), dim3((nt + 255) / 256), dim3(256), 0, s, x, (_Float16*)y, C, H, W,
+                 ps, GH, GW, nt);
+    else
+      SPI_LAUNCH((patchify_vec_kernel<float>), dim3((nt + 255) / 256), dim3(256), 0, s, x, (float*)y, C, H, W, ps, GH,
+                 GW, nt);
+    return;
+  }
   if (f16)
     SPI_LAUNCH((patchify_kernel<_Float16>), dim3(grid_for(n)), dim3(256), 0, s, x,
                        (_Float16*)y, B, C, H, W, ps);
