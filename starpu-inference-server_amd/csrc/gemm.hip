@@ -2275,6 +2275,7 @@ extern "C" void spi_debug_gemm_reload_env(void) {
   conv_wres_reload_env();
   gemm256_reload_env();
   attention_reload_env();
+  qkv_attn_reload_env();
 }
 
 // The plan gemm() would pick for a conv (tests: which kind runs): out[0..7] = bm, bn, stages,

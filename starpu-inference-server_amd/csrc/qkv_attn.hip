@@ -22,6 +22,7 @@
 #include "ln_fold.hpp"
 #include "spi_kernels.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace spi {
@@ -40,16 +41,19 @@ constexpr int LDQ = HD + 8;                 // Q / K / V row stride in elements 
 // Geometry by token rows per workgroup QR (S <= QR): one 64-deep k-step of A is QR x 128 bytes,
 // of W 192 x 128; 1 KiB LDS-DMA pieces per stage, per wave; Q / K / V over the ring after the
 // k-loop, the rows' {mean, rstd} (fold) after them.
-template <int QR>
+// HP heads per workgroup (round 6): 8 HP waves, the A rows staged once for the HP heads' W rows.
+template <int QR, int HP = 1>
 struct QkvGeo {
-  static constexpr int A_BYTES = QR * 128;          // 16 / 32 KiB
-  static constexpr int STAGE = A_BYTES + QC * 128;  // 40 / 56 KiB
-  static constexpr int PIECES = (QR + QC) / 8;      // 40 / 56
-  static constexpr int PPW = PIECES / 8;            // 5 / 7
-  static constexpr int QKV_BYTES = 3 * QR * LDQ * 2;
+  static constexpr int A_BYTES = QR * 128;               // 16 / 32 KiB
+  static constexpr int W_BYTES = QC * 128;               // one head's 192 W rows: 24 KiB
+  static constexpr int STAGE = A_BYTES + HP * W_BYTES;   // 40 / 56 KiB (HP 2: 64 KiB)
+  static constexpr int PIECES = (QR + HP * QC) / 8;      // 40 / 56 (HP 2: 64)
+  static constexpr int PPW = PIECES / (8 * HP);          // 5 / 7 (HP 2: 4)
+  static constexpr int HEAD_QKV = 3 * QR * LDQ * 2;      // one head's Q / K / V
+  static constexpr int QKV_BYTES = HP * HEAD_QKV;
   static constexpr int STATS_OFF = QKV_BYTES;
-  static constexpr int MI = QR / 32;                // 16-row fragments per wave (2 wave rows)
-  static_assert(PIECES % 8 == 0 && STATS_OFF + QR * 8 <= 2 * STAGE, "tile geometry");
+  static constexpr int MI = QR / 32;                     // 16-row fragments per wave (2 wave rows)
+  static_assert(PIECES % (8 * HP) == 0 && STATS_OFF + QR * 8 <= 2 * STAGE, "tile geometry");
 };
 
 struct QkvAttnArgs {
@@ -74,15 +78,19 @@ __device__ __forceinline__ void wait_vm_bar() {
 
 // STG ring stages: 3 (120 KiB, stage t + 2 in flight while t computes) or 2 (80 KiB: two
 // workgroups fit a CU)
-template <bool LNC, int STG, int QR>
-__global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
-  using Geo = QkvGeo<QR>;
+template <bool LNC, int STG, int QR, int HP = 1>
+__global__ __launch_bounds__(512 * HP) void qkv_attn_kernel(const QkvAttnArgs g) {
+  using Geo = QkvGeo<QR, HP>;
   constexpr int A_BYTES = Geo::A_BYTES, STAGE = Geo::STAGE, PPW = Geo::PPW, STATS_OFF = Geo::STATS_OFF;
   constexpr int MI = Geo::MI;
   __shared__ __attribute__((aligned(16))) char lds[STG * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x, lane = tid & 63, wave_g = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x / g.H, h = blockIdx.x - b * g.H;
+  // HP > 1: waves 8 hw .. 8 hw + 7 own head hw of the workgroup's HP (the loop below is the
+  // one-head kernel's, on the head's W image and Q / K / V region); the A pieces are shared
+  const int hw = wave_g >> 3, wave = wave_g & 7;
+  const int hgroups = g.H / HP;
+  const int b = blockIdx.x / hgroups, h0 = (blockIdx.x - b * hgroups) * HP, h = h0 + hw;
   const int S = g.S, D = g.H * HD;
   const size_t tok0 = (size_t)b * S;
 
@@ -94,14 +102,15 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
     const int rl = lane >> 3, chunk = (lane & 7) ^ rl;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-      const int pc = wave * PPW + j;
+      const int pc = wave_g * PPW + j;
       if (pc < QR / 8) {
         const int r = pc * 8 + rl;
         src[j] = reinterpret_cast<const char*>(g.A + (tok0 + min(r, S - 1)) * g.lda) + chunk * 16;
         dst[j] = pc * 1024;
       } else {
-        const int c = (pc - QR / 8) * 8 + rl;
-        const int wrow = (c >> 6) * D + h * HD + (c & 63);
+        const int cw = (pc - QR / 8) * 8 + rl;  // W image row: head cw / 192, column cw % 192
+        const int c = cw % QC;
+        const int wrow = (c >> 6) * D + (h0 + cw / QC) * HD + (c & 63);
         src[j] = reinterpret_cast<const char*>(g.W + (size_t)wrow * g.ldw) + chunk * 16;
         dst[j] = A_BYTES + (pc - QR / 8) * 1024;
       }
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) fa[kk][i] = rd(buf, (QR / 2) * wr + 16 * i + fr, kk * 4 + fq);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) fb[kk][j] = rd(buf + A_BYTES, 48 * wc + 16 * j + fr, kk * 4 + fq);
+      for (int j = 0; j < 3; ++j) fb[kk][j] = rd(buf + A_BYTES + hw * Geo::W_BYTES, 48 * wc + 16 * j + fr, kk * 4 + fq);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
   }
 
   // epilogue: acc[i][j][v] is row (QR / 2) wr + 16 i + 4 fq + v, tile column 48 wc + 16 j + fr
-  _Float16* const Qs = reinterpret_cast<_Float16*>(lds);
+  _Float16* const Qs = reinterpret_cast<_Float16*>(lds + hw * Geo::HEAD_QKV);
   _Float16* const Ks = Qs + QR * LDQ;
   _Float16* const Vs = Ks + QR * LDQ;
 #pragma unroll
@@ -306,6 +315,20 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(const QkvAttnArgs g) {
 
 constexpr int kQkvMaxS = 256;
 
+// SPI_QKV_HP=2: two heads per 16-wave workgroup for S <= 128 (the A rows staged once for both:
+// 20 % fewer bytes per head into LDS; 128 KiB, one workgroup per CU).  Bit-identical, but BERT-base
+// bs8 under the four streams 25.1k -> 24.2k (-3.7 %, profiles/r06/rejected/): a 16-wave, 128 KiB
+// workgroup waits for a whole free CU, so the default stays one head per workgroup
+static int g_qkv_hp = -1;
+void qkv_attn_reload_env() { g_qkv_hp = -1; }
+static int qkv_hp() {
+  if (g_qkv_hp < 0) {
+    const char* e = std::getenv("SPI_QKV_HP");
+    g_qkv_hp = (e && *e && std::atoi(e) == 2) ? 2 : 1;
+  }
+  return g_qkv_hp;
+}
+
 bool qkv_attention_eligible(int S, int heads, int hd, int K, int kpad, int krep, int lda, int ldw) {
   return S >= 1 && S <= kQkvMaxS && hd == HD && heads >= 2 && K == heads * HD && kpad == K && krep == 1 && K % 64 == 0 &&
          lda % 8 == 0 && ldw % 8 == 0;
@@ -340,7 +363,13 @@ void qkv_attention(const void* A, int lda, const void* W, int ldw, const float* 
   // two stages (QR 128: 80 KiB, two workgroups per CU): BERT-base bs8 four streams 24.7-24.8k
   // seq/s against 24.0k with three (120 KiB) and 23.3-23.4k unfused (profiles/r05/qkv_attn/);
   // sequences of 129..256 tokens (ViT at 197) take the 256-row tile (112 KiB)
-  if (S <= 128) {
+  if (S <= 128 && heads % 2 == 0 && qkv_hp() == 2) {
+    const dim3 grid2(B * heads / 2), blk2(1024);
+    if (ln_stats)
+      SPI_LAUNCH((qkv_attn_kernel<true, 2, 128, 2>), grid2, blk2, 0, s, g);
+    else
+      SPI_LAUNCH((qkv_attn_kernel<false, 2, 128, 2>), grid2, blk2, 0, s, g);
+  } else if (S <= 128) {
     if (ln_stats)
       SPI_LAUNCH((qkv_attn_kernel<true, 2, 128>), grid, blk, 0, s, g);
     else

@@ -167,6 +167,7 @@ bool conv_wres_eligible(const GemmDesc& d, Prec prec, const GemmPtrs& p);
 void conv_wres(const GemmDesc& d, const GemmPtrs& p, hipStream_t s);
 void conv_wres_reload_env();
 void attention_reload_env();  // SPI_ATTN_WHOLE
+void qkv_attn_reload_env();   // SPI_QKV_HP
 
 // NCHW fp32 image -> NHWC (compute type) with channels zero-padded to cpad.
 void ingest_nchw(const float* x, void* y, int B, int C, int H, int W, int cpad,

@@ -325,6 +325,30 @@ def test_bert_qkv_attention_fused(spi, zoo, gpu, S, pad_from, fold, monkeypatch)
 
 
 @pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("S,pad_from", [(128, None), (80, 50), (16, 9)])
+def test_bert_qkv_attention_two_heads_per_workgroup(spi, zoo, gpu, S, pad_from, fold, monkeypatch):
+    """SPI_QKV_HP=2 (round 6): two heads per 16-wave workgroup, the A rows staged once for both
+    heads' W rows; each head's arithmetic is the one-head kernel's, so the outputs are identical."""
+    rng = np.random.default_rng(41 + S)
+    m = zoo.bert(layers=2)
+    ids, mask = bert_inputs(rng, 3, S, pad_from=pad_from)
+    ref = cpu_inference(m, [ids, mask])[0]
+    monkeypatch.setenv("SPI_LN_FOLD", fold)
+    outs = {}
+    try:
+        for hp in ("2", "1"):
+            monkeypatch.setenv("SPI_QKV_HP", hp)
+            spi.lib.spi_debug_gemm_reload_env()
+            outs[hp] = hip_forward(spi, spi.ModelReplica(m, 0, "fp16", max_batch=3, seq_len=128), [ids, mask],
+                                   ref.shape)
+    finally:
+        monkeypatch.delenv("SPI_QKV_HP")
+        spi.lib.spi_debug_gemm_reload_env()
+    e = normalized_max_error(outs["2"], ref)
+    assert np.array_equal(outs["2"], outs["1"]) and e < 1e-3, e
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
 @pytest.mark.parametrize("img,patch", [(224, 16), (240, 16), (160, 16), (224, 14)])
 def test_vit_qkv_attention_fused(spi, zoo, gpu, img, patch, fold, monkeypatch):
     """The fused QKV projection + attention kernel on ViT (round 6: 256-row tiles for 129..256
